@@ -1,0 +1,746 @@
+// bdl_sgmcmc.hip — fused SG-MCMC parameter update for MI355X (gfx950, CDNA4).
+//
+// One bandwidth-bound sweep over flat fp32 vectors (parameters_to_vector order)
+// replaces the reference's per-tensor update loops plus torch.optim.SGD.step()
+// plus the thinned posterior-moment accumulation:
+//   cSGHMC  methods/csghmc.py:747-778  (+ Welford collect :327-345)
+//   SGHMC   methods/sghmc.py:482-510   (+ SGD momentum 0, :229; moments :242-249)
+//   SGLD    methods/sgld.py:469-484    (+ SGD momentum mu, :226; moments :239-246)
+//   cSGLD   methods/csgld.py:665-680   (+ SGD, :253; per-cycle moments :280-293)
+//
+// Design:
+//   * elementwise, HBM-bound: no LDS on the data stream, no MFMA; 16-B (dwordx4)
+//     loads/stores per lane, several independent float4 groups in flight per
+//     lane, each workgroup sweeps one contiguous span of the vector.
+//   * per-element attributes (lr group, prior on/off, skip) come from a tiny
+//     sorted run table; a block finds its first run with a block-uniform
+//     (scalar) binary search and each lane advances a cursor monotonically.
+//   * noise: either read from a buffer (torch-RNG parity mode) or generated in
+//     registers by counter-based Philox4x32-10 keyed by (seed, chain, step,
+//     element/4) + Box-Muller on v_log/v_sin/v_cos — no extra HBM traffic.
+//   * every floating-point op is rounded separately in the reference's order
+//     (compiled with -ffp-contract=off); SGD's add(alpha=-lr) is an explicit
+//     fmaf, as torch's CPU kernel computes it.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+
+#include "bdl_sgmcmc.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* msg) {
+  g_last_error = msg;
+  return code;
+}
+
+constexpr int kBlock = 256;  // 4 waves of 64 lanes
+
+// Tunables (bdl_set_launch_config).  blocks_per_cu * 256 CUs workgroups, each
+// lane keeps kUnroll float4 groups in flight per iteration.
+int g_blocks_per_cu = 4;
+int g_unroll = 2;
+
+int device_cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cached[dev] = cus;
+  }
+  return cached[dev];
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// ---------------------------------------------------------------------------
+// Counter-based RNG: Philox4x32-10 (Salmon et al., SC'11) + Box-Muller.
+// counter = (group index lo32, chain lo32, step lo32, step hi32), key = seed.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// uniform in (0, 1): 24 random bits, centred in their bucket -> never 0 or 1.
+__device__ __forceinline__ float u01(uint32_t x) {
+  return ((float)(x >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+// Four N(0,1) draws for flat elements 4*group .. 4*group+3.
+__device__ __forceinline__ float4 philox_normal4(uint64_t group, uint64_t seed, uint64_t chain,
+                                                  uint64_t step) {
+  const uint4 ctr = make_uint4((uint32_t)group, (uint32_t)chain, (uint32_t)step,
+                               (uint32_t)(step >> 32));
+  const uint4 r = philox4x32_10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+  // v_log_f32 is log2; v_sin_f32 / v_cos_f32 take the angle in revolutions,
+  // so sin(2*pi*u) is one instruction with no range reduction.
+  const float kM2Ln2 = -1.38629436111989061883f;  // -2 ln 2
+  const float ra = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(r.x)));
+  const float rb = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(r.z)));
+  const float ta = u01(r.y), tb = u01(r.w);
+  float4 z;
+  z.x = ra * __builtin_amdgcn_cosf(ta);
+  z.y = ra * __builtin_amdgcn_sinf(ta);
+  z.z = rb * __builtin_amdgcn_cosf(tb);
+  z.w = rb * __builtin_amdgcn_sinf(tb);
+  return z;
+}
+
+// ---------------------------------------------------------------------------
+// Vector helpers: a float4 "group" covers flat elements [4g, 4g+4).  Only the
+// very last group of a vector can be partial; it takes the guarded path.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float4 ld4(const float* __restrict__ p, int64_t e, int64_t n) {
+  if (e + 4 <= n) return *reinterpret_cast<const float4*>(p + e);
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e + 0 < n) v.x = p[e + 0];
+  if (e + 1 < n) v.y = p[e + 1];
+  if (e + 2 < n) v.z = p[e + 2];
+  return v;
+}
+
+__device__ __forceinline__ void st4(float* __restrict__ p, int64_t e, int64_t n, float4 v) {
+  if (e + 4 <= n) {
+    *reinterpret_cast<float4*>(p + e) = v;
+    return;
+  }
+  if (e + 0 < n) p[e + 0] = v.x;
+  if (e + 1 < n) p[e + 1] = v.y;
+  if (e + 2 < n) p[e + 2] = v.z;
+}
+
+__device__ __forceinline__ float& comp(float4& v, int j) {
+  return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+}
+
+// First run whose end is > idx (runs sorted by end, last end == n).
+__device__ __forceinline__ int find_run(const bdl_run* __restrict__ runs, int nruns, int64_t idx) {
+  int lo = 0, hi = nruns - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (runs[mid].end <= idx)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+struct KArgs {
+  float* __restrict__ theta;
+  float* __restrict__ grad;
+  float* __restrict__ mom;
+  const float* __restrict__ prior_mean;
+  const float* __restrict__ noise;
+  float* __restrict__ mom1;
+  float* __restrict__ mom2;
+  const bdl_run* __restrict__ runs;
+  int32_t nruns;
+  int32_t flags;
+  int64_t n;
+  int64_t groups_per_block;
+  float lr0, lr1, ns0, ns1;
+  float one_minus_alpha, prior_sig, sigma2, n_data, mu, ca, cb;
+  uint64_t seed, chain, step;
+};
+
+// Scalar division in the reference's rounding: torch CPU divides (x / s);
+// torch on a HIP device multiplies by the fp32 reciprocal (x * fl(1/s)).
+template <bool RECIP>
+__device__ __forceinline__ float sdiv(float x, float s, float inv_s) {
+  if constexpr (RECIP)
+    return x * inv_s;
+  else
+    return x / s;
+}
+
+// ---------------------------------------------------------------------------
+// Per-element update.  All arithmetic is separately rounded fp32 in exactly
+// the reference's op order (the file is compiled with -ffp-contract=off).
+// ---------------------------------------------------------------------------
+template <int METHOD, int NOISE, int COLLECT, bool RECIP>
+__device__ __forceinline__ void update_elem(const KArgs& a, uint32_t attr, float& th, float& g,
+                                            float& v, float th0, float eps, float& m1, float& m2,
+                                            float inv_s2, float inv_nd, float inv_ca,
+                                            float inv_cb) {
+  const bool head = (attr & BDL_ATTR_HEAD) != 0;
+  const bool skip = (attr & BDL_ATTR_SKIP) != 0;
+  const float eta = head ? a.lr1 : a.lr0;
+  const float ns = head ? a.ns1 : a.ns0;
+
+  if (!skip) {
+    if constexpr (METHOD == BDL_CSGHMC) {
+      // csghmc.py:759-762 — both branches are grad + prior_sig * theta (Q1)
+      const float t = a.prior_sig * th;
+      const float gU = g + t;
+      const float x = v * a.one_minus_alpha;  // :770 v*(1-a)
+      const float y = eta * gU;               //      lr*grad_U
+      float vn = x - y;
+      if constexpr (NOISE != BDL_NOISE_NONE) vn = vn + ns * eps;  // + noise (:765-770)
+      v = vn;                                 // :775
+      th = th + vn;                           // :778 p.data.add_(v)
+    } else if constexpr (METHOD == BDL_SGHMC || METHOD == BDL_SGHMC_GRAD) {
+      float gU = g;  // sghmc.py:494-497
+      if (attr & BDL_ATTR_PRIOR) {
+        const float d = th - th0;
+        const float e = sdiv<RECIP>(d, a.sigma2, inv_s2);
+        gU = g + sdiv<RECIP>(e, a.n_data, inv_nd);
+      }
+      const float s = v * a.one_minus_alpha + eta * gU;  // :504 (two products rounded)
+      const float vn = s + ns * eps;
+      const float gp = g + vn;  // :510 p.grad = p.grad + v
+      v = vn;
+      if constexpr (METHOD == BDL_SGHMC) {
+        th = fmaf(-eta, gp, th);  // SGD(momentum=0): param.add_(grad, alpha=-lr)
+      } else {
+        g = gp;
+      }
+    } else {  // BDL_SGLD / BDL_SGLD_GRAD  (sgld.py:471-484)
+      const float nz = ns * eps;
+      float gp;
+      if (attr & BDL_ATTR_PRIOR) {
+        const float d = th - th0;
+        const float e = sdiv<RECIP>(d, a.sigma2, inv_s2);
+        const float f = sdiv<RECIP>(e, a.n_data, inv_nd);
+        gp = g + (f + nz);
+      } else {
+        gp = g + nz;
+      }
+      if constexpr (METHOD == BDL_SGLD) {
+        float stepv = gp;
+        if (a.flags & BDL_FLAG_MOMENTUM) {  // torch SGD momentum buffer
+          v = (a.flags & BDL_FLAG_FIRST_STEP) ? gp : (a.mu * v + gp);
+          stepv = v;
+        }
+        th = fmaf(-eta, stepv, th);
+      } else {
+        g = gp;
+      }
+    }
+  }
+
+  // Posterior moments on the updated theta (parameters_to_vector after step).
+  if constexpr (COLLECT == BDL_COLLECT_WELFORD_INIT) {
+    m1 = th;
+    m2 = 0.0f;
+  } else if constexpr (COLLECT == BDL_COLLECT_WELFORD) {
+    const float d = th - m1;
+    m1 = m1 + sdiv<RECIP>(d, a.ca, inv_ca);
+    const float d2 = th - m1;
+    m2 = m2 + d * d2;
+  } else if constexpr (COLLECT == BDL_COLLECT_MEAN_INIT) {
+    m1 = th;
+    m2 = th * th;
+  } else if constexpr (COLLECT == BDL_COLLECT_MEAN) {
+    m1 = sdiv<RECIP>(th + a.ca * m1, a.cb, inv_cb);
+    m2 = sdiv<RECIP>(th * th + a.ca * m2, a.cb, inv_cb);
+  }
+}
+
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
+__device__ __forceinline__ void step_body(const KArgs& a) {
+  constexpr bool kReadPrior = (METHOD != BDL_CSGHMC);
+  constexpr bool kMom =
+      (METHOD == BDL_CSGHMC || METHOD == BDL_SGHMC || METHOD == BDL_SGHMC_GRAD);
+  constexpr bool kWriteTheta = (METHOD == BDL_CSGHMC || METHOD == BDL_SGHMC || METHOD == BDL_SGLD);
+  constexpr bool kWriteGrad = (METHOD == BDL_SGHMC_GRAD || METHOD == BDL_SGLD_GRAD);
+  constexpr bool kCollect = (COLLECT != BDL_COLLECT_NONE);
+  constexpr bool kReadMoments = (COLLECT == BDL_COLLECT_WELFORD || COLLECT == BDL_COLLECT_MEAN);
+
+  const bool sgd_mom = (METHOD == BDL_SGLD) && (a.flags & BDL_FLAG_MOMENTUM);
+  const bool sgd_mom_read = sgd_mom && !(a.flags & BDL_FLAG_FIRST_STEP);
+  const bool has_m2 = kCollect && (a.mom2 != nullptr);
+
+  const float inv_s2 = 1.0f / a.sigma2;
+  const float inv_nd = 1.0f / a.n_data;
+  const float inv_ca = 1.0f / a.ca;
+  const float inv_cb = 1.0f / a.cb;
+
+  const int64_t n = a.n;
+  const int64_t ngroups = (n + 3) >> 2;
+  const int64_t g0 = (int64_t)blockIdx.x * a.groups_per_block;
+  const int64_t g1 = min(g0 + a.groups_per_block, ngroups);
+  if (g0 >= g1) return;
+
+  // Block-uniform run search for the span start; each lane then advances.
+  int r = find_run(a.runs, a.nruns, g0 * 4);
+  int64_t run_hi = a.runs[r].end;
+  uint32_t run_attr = a.runs[r].attr;
+
+  for (int64_t gb = g0; gb < g1; gb += (int64_t)kBlock * UNROLL) {
+    float4 th[UNROLL], g[UNROLL], v[UNROLL], t0[UNROLL], ep[UNROLL], m1[UNROLL], m2[UNROLL];
+    int64_t e[UNROLL];
+    bool act[UNROLL];
+
+    // ---- issue every load of this iteration before any arithmetic ----
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+      act[u] = gi < g1;
+      e[u] = gi * 4;
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      th[u] = g[u] = v[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
+      if (act[u]) {
+        th[u] = ld4(a.theta, e[u], n);
+        g[u] = ld4(a.grad, e[u], n);
+        if (kMom || sgd_mom_read) v[u] = ld4(a.mom, e[u], n);
+        if (kReadPrior) t0[u] = ld4(a.prior_mean, e[u], n);
+        if (NOISE == BDL_NOISE_BUFFER) ep[u] = ld4(a.noise, e[u], n);
+        if (kReadMoments) {
+          m1[u] = ld4(a.mom1, e[u], n);
+          if (has_m2) m2[u] = ld4(a.mom2, e[u], n);
+        }
+      }
+    }
+
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      if (!act[u]) continue;
+      if constexpr (NOISE == BDL_NOISE_PHILOX)
+        ep[u] = philox_normal4((uint64_t)(e[u] >> 2), a.seed, a.chain, a.step);
+
+      // attributes: fast path when the whole group sits in the cursor's run
+      while (run_hi <= e[u] && r < a.nruns - 1) {
+        ++r;
+        run_hi = a.runs[r].end;
+        run_attr = a.runs[r].attr;
+      }
+      uint32_t at[4] = {run_attr, run_attr, run_attr, run_attr};
+      if (e[u] + 4 > run_hi) {  // group straddles a run boundary (rare)
+        int rr = r;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          while (rr < a.nruns - 1 && a.runs[rr].end <= e[u] + j) ++rr;
+          at[j] = a.runs[rr].attr;
+        }
+      }
+
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        update_elem<METHOD, NOISE, COLLECT, RECIP>(a, at[j], comp(th[u], j), comp(g[u], j),
+                                                   comp(v[u], j), comp(t0[u], j), comp(ep[u], j),
+                                                   comp(m1[u], j), comp(m2[u], j), inv_s2, inv_nd,
+                                                   inv_ca, inv_cb);
+      }
+
+      if (kWriteTheta) st4(a.theta, e[u], n, th[u]);
+      if (kWriteGrad) st4(a.grad, e[u], n, g[u]);
+      if (kMom || sgd_mom) st4(a.mom, e[u], n, v[u]);
+      if (kCollect) {
+        st4(a.mom1, e[u], n, m1[u]);
+        if (has_m2) st4(a.mom2, e[u], n, m2[u]);
+      }
+    }
+  }
+}
+
+template <int METHOD, int NOISE, int COLLECT, int UNROLL>
+__global__ __launch_bounds__(kBlock) void bdl_step_kernel(const KArgs a) {
+  if (a.flags & BDL_FLAG_RECIP_DIV)
+    step_body<METHOD, NOISE, COLLECT, true, UNROLL>(a);
+  else
+    step_body<METHOD, NOISE, COLLECT, false, UNROLL>(a);
+}
+
+// ---------------------------------------------------------------------------
+// Stand-alone moments, posterior sample, raw Philox stream.
+// ---------------------------------------------------------------------------
+struct MArgs {
+  const float* __restrict__ theta;
+  float* __restrict__ mom1;
+  float* __restrict__ mom2;
+  int64_t n;
+  int32_t collect;
+  int32_t recip;
+  float ca, cb;
+};
+
+__global__ __launch_bounds__(kBlock) void bdl_moments_kernel(const MArgs a) {
+  const int64_t ngroups = (a.n + 3) >> 2;
+  const float inv_ca = 1.0f / a.ca, inv_cb = 1.0f / a.cb;
+  for (int64_t gi = (int64_t)blockIdx.x * kBlock + threadIdx.x; gi < ngroups;
+       gi += (int64_t)gridDim.x * kBlock) {
+    const int64_t e = gi * 4;
+    float4 t = ld4(a.theta, e, a.n), m1 = make_float4(0, 0, 0, 0), m2 = m1;
+    if (a.collect == BDL_COLLECT_WELFORD || a.collect == BDL_COLLECT_MEAN) {
+      m1 = ld4(a.mom1, e, a.n);
+      if (a.mom2) m2 = ld4(a.mom2, e, a.n);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = comp(t, j);
+      float& p = comp(m1, j);
+      float& q = comp(m2, j);
+      switch (a.collect) {
+        case BDL_COLLECT_WELFORD_INIT:
+          p = x;
+          q = 0.f;
+          break;
+        case BDL_COLLECT_WELFORD: {
+          const float d = x - p;
+          p = p + (a.recip ? d * inv_ca : d / a.ca);
+          const float d2 = x - p;
+          q = q + d * d2;
+          break;
+        }
+        case BDL_COLLECT_MEAN_INIT:
+          p = x;
+          q = x * x;
+          break;
+        default: {  // MEAN
+          const float u = x + a.ca * p;
+          p = a.recip ? u * inv_cb : u / a.cb;
+          const float w = x * x + a.ca * q;
+          q = a.recip ? w * inv_cb : w / a.cb;
+        }
+      }
+    }
+    st4(a.mom1, e, a.n, m1);
+    if (a.mom2) st4(a.mom2, e, a.n, m2);
+  }
+}
+
+struct SArgs {
+  float* __restrict__ out;
+  const float* __restrict__ mom1;
+  const float* __restrict__ mom2;
+  const float* __restrict__ noise;
+  int64_t n;
+  int32_t var_mode, noise_mode;
+  float ratio, var_floor;
+  uint64_t seed, chain, step;
+};
+
+__global__ __launch_bounds__(kBlock) void bdl_sample_kernel(const SArgs a) {
+  const int64_t ngroups = (a.n + 3) >> 2;
+  for (int64_t gi = (int64_t)blockIdx.x * kBlock + threadIdx.x; gi < ngroups;
+       gi += (int64_t)gridDim.x * kBlock) {
+    const int64_t e = gi * 4;
+    const float4 m = ld4(a.mom1, e, a.n);
+    float4 q = make_float4(0, 0, 0, 0);
+    if (a.mom2) q = ld4(a.mom2, e, a.n);
+    float4 eps = (a.noise_mode == BDL_NOISE_BUFFER) ? ld4(a.noise, e, a.n)
+                                                    : philox_normal4((uint64_t)gi, a.seed, a.chain,
+                                                                     a.step);
+    float4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float mj = comp(const_cast<float4&>(m), j);
+      const float qj = comp(q, j);
+      float var;
+      if (!a.mom2)
+        var = a.var_floor;  // single-sample cycle: ones*1e-12 (csghmc.py:456-458)
+      else if (a.var_mode == BDL_VAR_RAW_MOMENTS)
+        var = a.ratio * (qj - mj * mj);  // sgld.py:342
+      else if (a.var_mode == BDL_VAR_WELFORD)
+        var = qj / a.ratio;  // csghmc.py:455
+      else
+        var = qj;
+      if (!(var != var)) var = fmaxf(var, a.var_floor);  // clamp_(min=1e-12); NaN stays NaN
+      comp(o, j) = mj + sqrtf(var) * comp(eps, j);  // p_m + p_v.sqrt()*eps
+    }
+    st4(a.out, e, a.n, o);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void bdl_philox_kernel(float* __restrict__ out, int64_t n,
+                                                            uint64_t seed, uint64_t chain,
+                                                            uint64_t step) {
+  const int64_t ngroups = (n + 3) >> 2;
+  for (int64_t gi = (int64_t)blockIdx.x * kBlock + threadIdx.x; gi < ngroups;
+       gi += (int64_t)gridDim.x * kBlock) {
+    st4(out, gi * 4, n, philox_normal4((uint64_t)gi, seed, chain, step));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Dispatch
+// ---------------------------------------------------------------------------
+using StepKernel = void (*)(const KArgs);
+
+template <int METHOD, int NOISE, int COLLECT>
+StepKernel pick_unroll(int unroll) {
+  // Only the cSGHMC (headline) kernel is instantiated at every unroll depth;
+  // the other methods use the default depth to keep build time down.
+  if constexpr (METHOD != BDL_CSGHMC) {
+    (void)unroll;
+    return bdl_step_kernel<METHOD, NOISE, COLLECT, 2>;
+  } else {
+    switch (unroll) {
+      case 1:
+        return bdl_step_kernel<METHOD, NOISE, COLLECT, 1>;
+      case 4:
+        return bdl_step_kernel<METHOD, NOISE, COLLECT, 4>;
+      default:
+        return bdl_step_kernel<METHOD, NOISE, COLLECT, 2>;
+    }
+  }
+}
+
+template <int METHOD, int NOISE>
+StepKernel pick_collect(int collect, int unroll) {
+  switch (collect) {
+    case BDL_COLLECT_NONE:
+      return pick_unroll<METHOD, NOISE, BDL_COLLECT_NONE>(unroll);
+    case BDL_COLLECT_WELFORD_INIT:
+      return pick_unroll<METHOD, NOISE, BDL_COLLECT_WELFORD_INIT>(unroll);
+    case BDL_COLLECT_WELFORD:
+      return pick_unroll<METHOD, NOISE, BDL_COLLECT_WELFORD>(unroll);
+    case BDL_COLLECT_MEAN_INIT:
+      return pick_unroll<METHOD, NOISE, BDL_COLLECT_MEAN_INIT>(unroll);
+    case BDL_COLLECT_MEAN:
+      return pick_unroll<METHOD, NOISE, BDL_COLLECT_MEAN>(unroll);
+  }
+  return nullptr;
+}
+
+template <int METHOD>
+StepKernel pick_noise(int noise, int collect, int unroll) {
+  switch (noise) {
+    case BDL_NOISE_NONE:
+      return pick_collect<METHOD, BDL_NOISE_NONE>(collect, unroll);
+    case BDL_NOISE_BUFFER:
+      return pick_collect<METHOD, BDL_NOISE_BUFFER>(collect, unroll);
+    case BDL_NOISE_PHILOX:
+      return pick_collect<METHOD, BDL_NOISE_PHILOX>(collect, unroll);
+  }
+  return nullptr;
+}
+
+StepKernel pick_step(int method, int noise, int collect, int unroll) {
+  switch (method) {
+    case BDL_CSGHMC:
+      return pick_noise<BDL_CSGHMC>(noise, collect, unroll);
+    case BDL_SGHMC:
+      return pick_noise<BDL_SGHMC>(noise, collect, unroll);
+    case BDL_SGLD:
+      return pick_noise<BDL_SGLD>(noise, collect, unroll);
+    case BDL_SGHMC_GRAD:
+      return collect == BDL_COLLECT_NONE ? pick_noise<BDL_SGHMC_GRAD>(noise, BDL_COLLECT_NONE, unroll)
+                                         : nullptr;
+    case BDL_SGLD_GRAD:
+      return collect == BDL_COLLECT_NONE ? pick_noise<BDL_SGLD_GRAD>(noise, BDL_COLLECT_NONE, unroll)
+                                         : nullptr;
+  }
+  return nullptr;
+}
+
+int grid_for(int64_t ngroups, int per_block_groups) {
+  const int64_t want = (ngroups + per_block_groups - 1) / per_block_groups;
+  const int64_t cap = (int64_t)device_cu_count() * 8;
+  return (int)std::max<int64_t>(1, std::min(want, cap));
+}
+
+}  // namespace
+
+extern "C" {
+
+int bdl_version(void) { return BDL_ABI_VERSION; }
+
+const char* bdl_last_error(void) { return g_last_error.c_str(); }
+
+int bdl_set_launch_config(int32_t blocks_per_cu, int32_t unroll) {
+  const int prev = (g_blocks_per_cu << 16) | g_unroll;
+  g_blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : 4;
+  g_unroll = (unroll == 1 || unroll == 2 || unroll == 4) ? unroll : 2;
+  return prev;
+}
+
+int bdl_build_runs(const bdl_segment* segs, int32_t nseg, int64_t n, bdl_run* out, int32_t max_runs) {
+  if (!out || (nseg > 0 && !segs)) return fail(BDL_ERR_NULL, "bdl_build_runs: null pointer");
+  if (n < 0 || nseg < 0 || max_runs < 1) return fail(BDL_ERR_ARG, "bdl_build_runs: bad sizes");
+  int nr = 0;
+  int64_t pos = 0;
+  auto push = [&](int64_t end, uint32_t attr) -> bool {
+    if (end <= pos) return true;
+    if (nr > 0 && out[nr - 1].attr == attr) {
+      out[nr - 1].end = end;
+    } else {
+      if (nr >= max_runs) return false;
+      out[nr].end = end;
+      out[nr].attr = attr;
+      out[nr].pad = 0;
+      ++nr;
+    }
+    pos = end;
+    return true;
+  };
+  for (int i = 0; i < nseg; ++i) {
+    const bdl_segment& s = segs[i];
+    if (s.offset < pos || s.numel < 0 || s.offset + s.numel > n)
+      return fail(BDL_ERR_RUNS, "bdl_build_runs: segments overlap, are unsorted or exceed n");
+    if (!push(s.offset, BDL_ATTR_SKIP)) return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
+    if (!push(s.offset + s.numel, s.attr & 7u))
+      return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
+  }
+  if (!push(n, BDL_ATTR_SKIP)) return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
+  if (nr == 0) {  // n == 0: one empty run keeps the table well-formed
+    out[0].end = 0;
+    out[0].attr = BDL_ATTR_SKIP;
+    out[0].pad = 0;
+    nr = 1;
+  }
+  return nr;
+}
+
+int bdl_sgmcmc_step(const bdl_step_args* s, void* stream) {
+  if (!s) return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: null args");
+  if (s->n < 0) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: n < 0");
+  if (s->method < BDL_CSGHMC || s->method > BDL_SGLD_GRAD)
+    return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: unknown method");
+  if (s->noise_mode < BDL_NOISE_NONE || s->noise_mode > BDL_NOISE_PHILOX)
+    return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: unknown noise mode");
+  if (s->collect < BDL_COLLECT_NONE || s->collect > BDL_COLLECT_MEAN)
+    return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: unknown collect mode");
+  if (s->n == 0) return BDL_OK;
+  const bool grad_only = s->method == BDL_SGHMC_GRAD || s->method == BDL_SGLD_GRAD;
+  const bool needs_mom = s->method == BDL_CSGHMC || s->method == BDL_SGHMC ||
+                         s->method == BDL_SGHMC_GRAD ||
+                         (s->method == BDL_SGLD && (s->flags & BDL_FLAG_MOMENTUM));
+  const bool needs_prior = s->method != BDL_CSGHMC;
+  if (!s->theta || !s->grad || !s->runs || s->nruns < 1)
+    return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: theta, grad and runs are required");
+  if (needs_mom && !s->mom) return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: mom is required");
+  if (needs_prior && !s->prior_mean)
+    return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: prior_mean is required for sghmc/sgld");
+  if (s->noise_mode == BDL_NOISE_BUFFER && !s->noise)
+    return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: noise buffer is required");
+  if (s->collect != BDL_COLLECT_NONE && !s->mom1)
+    return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: mom1 is required to collect");
+  if (grad_only && s->collect != BDL_COLLECT_NONE)
+    return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: grad-only methods cannot collect");
+  const void* ptrs[] = {s->theta, s->grad, s->mom, s->prior_mean, s->noise, s->mom1, s->mom2};
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_sgmcmc_step: vector not 16-B aligned");
+
+  const int unroll = g_unroll;
+  StepKernel k = pick_step(s->method, s->noise_mode, s->collect, unroll);
+  if (!k) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: unsupported method/noise/collect combination");
+
+  const int64_t ngroups = (s->n + 3) / 4;
+  const int64_t per_iter = (int64_t)kBlock * unroll;
+  const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
+  int64_t iters = (ngroups + per_iter - 1) / per_iter;
+  int64_t grid = std::max<int64_t>(1, std::min(iters, cap));
+  int64_t iters_per_block = (iters + grid - 1) / grid;
+  grid = (iters + iters_per_block - 1) / iters_per_block;
+
+  KArgs a;
+  a.theta = s->theta;
+  a.grad = s->grad;
+  a.mom = s->mom;
+  a.prior_mean = s->prior_mean;
+  a.noise = s->noise;
+  a.mom1 = s->mom1;
+  a.mom2 = s->mom2;
+  a.runs = s->runs;
+  a.nruns = s->nruns;
+  a.flags = s->flags;
+  a.n = s->n;
+  a.groups_per_block = iters_per_block * per_iter;
+  a.lr0 = s->lr[0];
+  a.lr1 = s->lr[1];
+  a.ns0 = s->noise_scale[0];
+  a.ns1 = s->noise_scale[1];
+  a.one_minus_alpha = s->one_minus_alpha;
+  a.prior_sig = s->prior_sig;
+  a.sigma2 = s->sigma2;
+  a.n_data = s->n_data;
+  a.mu = s->mu;
+  a.ca = s->collect_a;
+  a.cb = s->collect_b;
+  a.seed = s->seed;
+  a.chain = s->chain;
+  a.step = s->step;
+
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)stream, a);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    g_last_error = std::string("bdl_sgmcmc_step: launch failed: ") + hipGetErrorString(err);
+    return BDL_ERR_LAUNCH;
+  }
+  return BDL_OK;
+}
+
+int bdl_moments_update(const bdl_moments_args* m, void* stream) {
+  if (!m) return fail(BDL_ERR_NULL, "bdl_moments_update: null args");
+  if (m->n < 0 || m->collect < BDL_COLLECT_WELFORD_INIT || m->collect > BDL_COLLECT_MEAN)
+    return fail(BDL_ERR_ARG, "bdl_moments_update: bad n or collect mode");
+  if (m->n == 0) return BDL_OK;
+  if (!m->theta || !m->mom1) return fail(BDL_ERR_NULL, "bdl_moments_update: theta/mom1 required");
+  const void* ptrs[] = {m->theta, m->mom1, m->mom2};
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_moments_update: vector not 16-B aligned");
+  MArgs a{m->theta, m->mom1, m->mom2, m->n, m->collect, (m->flags & BDL_FLAG_RECIP_DIV) ? 1 : 0,
+          m->collect_a, m->collect_b};
+  hipLaunchKernelGGL(bdl_moments_kernel, dim3(grid_for((m->n + 3) / 4, kBlock * 4)), dim3(kBlock), 0,
+                     (hipStream_t)stream, a);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    g_last_error = std::string("bdl_moments_update: launch failed: ") + hipGetErrorString(err);
+    return BDL_ERR_LAUNCH;
+  }
+  return BDL_OK;
+}
+
+int bdl_posterior_sample(const bdl_sample_args* s, void* stream) {
+  if (!s) return fail(BDL_ERR_NULL, "bdl_posterior_sample: null args");
+  if (s->n < 0 || s->var_mode < BDL_VAR_GIVEN || s->var_mode > BDL_VAR_WELFORD ||
+      (s->noise_mode != BDL_NOISE_BUFFER && s->noise_mode != BDL_NOISE_PHILOX))
+    return fail(BDL_ERR_ARG, "bdl_posterior_sample: bad arguments");
+  if (s->n == 0) return BDL_OK;
+  if (!s->out || !s->mom1 || (s->noise_mode == BDL_NOISE_BUFFER && !s->noise))
+    return fail(BDL_ERR_NULL, "bdl_posterior_sample: out, mom1 (and noise) required");
+  const void* ptrs[] = {s->out, s->mom1, s->mom2, s->noise};
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_posterior_sample: vector not 16-B aligned");
+  SArgs a{s->out, s->mom1, s->mom2, s->noise, s->n, s->var_mode, s->noise_mode,
+          s->ratio, s->var_floor, s->seed, s->chain, s->step};
+  hipLaunchKernelGGL(bdl_sample_kernel, dim3(grid_for((s->n + 3) / 4, kBlock * 4)), dim3(kBlock), 0,
+                     (hipStream_t)stream, a);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    g_last_error = std::string("bdl_posterior_sample: launch failed: ") + hipGetErrorString(err);
+    return BDL_ERR_LAUNCH;
+  }
+  return BDL_OK;
+}
+
+int bdl_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t chain, uint64_t step,
+                      void* stream) {
+  if (n < 0) return fail(BDL_ERR_ARG, "bdl_philox_normal: n < 0");
+  if (n == 0) return BDL_OK;
+  if (!out) return fail(BDL_ERR_NULL, "bdl_philox_normal: null out");
+  if (!aligned16(out)) return fail(BDL_ERR_ALIGN, "bdl_philox_normal: out not 16-B aligned");
+  hipLaunchKernelGGL(bdl_philox_kernel, dim3(grid_for((n + 3) / 4, kBlock * 4)), dim3(kBlock), 0,
+                     (hipStream_t)stream, out, n, seed, chain, step);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    g_last_error = std::string("bdl_philox_normal: launch failed: ") + hipGetErrorString(err);
+    return BDL_ERR_LAUNCH;
+  }
+  return BDL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,216 @@
+/*
+ * bdl_sgmcmc.h — C-ABI of the MI355X-native fused SG-MCMC parameter update.
+ *
+ * This is the drop-in boundary for the per-step update of the reference's
+ * methods/{csghmc,sghmc,csgld,sgld}.py Runner/Model step loop.  The Python host
+ * package (bayesdll_amd) binds these symbols with ctypes; any other host
+ * (C, C++, another FFI) can bind them the same way — no torch types cross
+ * this boundary, only plain device pointers, sizes and scalars.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference repo root):
+ *
+ *   bdl_sgmcmc_step  replaces, in one launch over flat fp32 vectors,
+ *     - methods/csghmc.py:747-778  per-tensor cSGHMC momentum + theta update
+ *     - methods/sghmc.py:482-510   SGHMC grad_U / momentum / p.grad = g + v
+ *       followed by torch.optim.SGD(momentum=0).step()  (methods/sghmc.py:229)
+ *     - methods/sgld.py:469-484    SGLD p.grad = g + prior + noise
+ *       followed by torch.optim.SGD(momentum=mu).step() (methods/sgld.py:226)
+ *     - methods/csgld.py:665-680   same as sgld under the cyclical lr
+ *       (methods/csgld.py:253 for the SGD step)
+ *     - the posterior-moment accumulation that follows on thinned steps:
+ *       methods/csghmc.py:327-345 (Welford), methods/sgld.py:239-246 and
+ *       methods/sghmc.py:242-249 (running mean), methods/csgld.py:280-293
+ *       (per-cycle running mean)
+ *   bdl_moments_update replaces the stand-alone moment updates
+ *     (methods/sgld.py:95-102 burn-in seeding; the same formulas as above
+ *     when the caller does not fuse them into the step).
+ *   bdl_posterior_sample replaces the per-tensor posterior draw
+ *     p.copy_(mean + var.sqrt() * randn_like(p))  (methods/sgld.py:292-296,
+ *     methods/csghmc.py:466-468) and the variance-from-moments formulas
+ *     (methods/sgld.py:337-345, methods/csghmc.py:451-459).
+ *   bdl_philox_normal exposes the in-kernel N(0,1) generator (the stream the
+ *     step kernel uses in BDL_NOISE_PHILOX mode), replacing torch.randn_like
+ *     (methods/csghmc.py:766) for statistical testing and host inspection.
+ *   bdl_build_runs is host-only: it turns the per-tensor segment table
+ *     (named_parameters order, readout_name, 'bias' names — the selection
+ *     logic of methods/csghmc.py:750-762 / methods/sgld.py:471-484) into the
+ *     merged run table the kernels read.
+ *
+ * Conventions
+ *   - Return 0 on success, a negative bdl_status on failure; a thread-local
+ *     message is available through bdl_last_error().  No exception crosses
+ *     the ABI.
+ *   - All vector pointers are device pointers (hipMalloc / torch HIP tensors),
+ *     16-byte aligned, fp32, contiguous, n elements, in the canonical flat
+ *     order of nn.utils.parameters_to_vector(net.parameters()).
+ *   - Launches are asynchronous on the given hipStream_t (pass torch's
+ *     current stream); no host synchronisation, no allocation.
+ */
+#ifndef BDL_SGMCMC_H
+#define BDL_SGMCMC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BDL_ABI_VERSION 1
+
+typedef enum bdl_status {
+  BDL_OK = 0,
+  BDL_ERR_NULL = -1,       /* a required pointer is null                    */
+  BDL_ERR_ALIGN = -2,      /* a vector pointer is not 16-byte aligned        */
+  BDL_ERR_ARG = -3,        /* inconsistent sizes / enum out of range         */
+  BDL_ERR_LAUNCH = -4,     /* HIP launch error                               */
+  BDL_ERR_RUNS = -5        /* run table does not cover [0, n) monotonically  */
+} bdl_status;
+
+/* Which update rule (and which reference code path) a step applies. */
+typedef enum bdl_method {
+  BDL_CSGHMC = 0,      /* methods/csghmc.py:747-778; theta and mom updated    */
+  BDL_SGHMC = 1,       /* methods/sghmc.py:482-510 + SGD(momentum 0) step     */
+  BDL_SGLD = 2,        /* methods/sgld.py:469-484 (and csgld) + SGD(mu) step  */
+  BDL_SGHMC_GRAD = 3,  /* sghmc Model.forward only: grad <- g + v', mom <- v' */
+  BDL_SGLD_GRAD = 4    /* sgld Model.forward only: grad <- g + prior + noise  */
+} bdl_method;
+
+typedef enum bdl_noise_mode {
+  BDL_NOISE_NONE = 0,    /* no noise term (cSGHMC exploration steps)          */
+  BDL_NOISE_BUFFER = 1,  /* eps read from args.noise (torch-RNG parity mode)  */
+  BDL_NOISE_PHILOX = 2   /* eps from in-kernel Philox4x32-10 + Box-Muller     */
+} bdl_noise_mode;
+
+/* Posterior-moment accumulation fused after the update (on the new theta). */
+typedef enum bdl_collect {
+  BDL_COLLECT_NONE = 0,
+  BDL_COLLECT_WELFORD_INIT = 1, /* m1 = theta, m2 = 0    (csghmc.py:333-337)  */
+  BDL_COLLECT_WELFORD = 2,      /* d=t-m1; m1+=d/a; d2=t-m1; m2+=d*d2 (:340-345) */
+  BDL_COLLECT_MEAN_INIT = 3,    /* m1 = theta, m2 = theta^2 (csgld.py:282-284)  */
+  BDL_COLLECT_MEAN = 4          /* m = (x + a*m) / b, x in {t, t^2} (sgld.py:242-245) */
+} bdl_collect;
+
+/* Per-element attribute bits carried by a run. */
+#define BDL_ATTR_HEAD 0x1     /* readout_name in pname -> lr group 1          */
+#define BDL_ATTR_PRIOR 0x2    /* prior term applied (not an uninformative bias)*/
+#define BDL_ATTR_SKIP 0x4     /* parameter has no grad: left untouched          */
+
+/* Flags for bdl_step_args.flags. */
+#define BDL_FLAG_FIRST_STEP 0x1  /* SGD momentum buffer does not exist yet: buf = grad */
+#define BDL_FLAG_RECIP_DIV 0x2   /* divide by a scalar as x*(1/s) (torch-on-GPU), else x/s (torch CPU) */
+#define BDL_FLAG_MOMENTUM 0x4    /* SGD momentum != 0: maintain args.mom as SGD buffer */
+
+/* One parameter tensor in named_parameters order (host input to bdl_build_runs). */
+typedef struct bdl_segment {
+  int64_t offset;   /* element offset in the flat vector                      */
+  int64_t numel;    /* element count                                          */
+  uint32_t attr;    /* BDL_ATTR_* bits                                        */
+  uint32_t pad;
+} bdl_segment;
+
+/* A maximal run of consecutive elements with identical attributes.
+ * Runs are sorted; run i covers [runs[i-1].end, runs[i].end). Device-resident. */
+typedef struct bdl_run {
+  int64_t end;
+  uint32_t attr;
+  uint32_t pad;
+} bdl_run;
+
+typedef struct bdl_step_args {
+  /* vectors (device, fp32, n elements) */
+  float* theta;            /* in/out                                               */
+  float* grad;             /* in (out for *_GRAD methods)                           */
+  float* mom;              /* csghmc/sghmc momentum v, or SGD momentum buffer       */
+  const float* prior_mean; /* theta0 (sghmc/sgld); may be null for csghmc           */
+  const float* noise;      /* BDL_NOISE_BUFFER only                                 */
+  float* mom1;             /* collect only                                          */
+  float* mom2;             /* collect only; may be null (nst == 0)                  */
+  const bdl_run* runs;     /* device run table                                      */
+  int32_t nruns;
+  int32_t method;          /* bdl_method      */
+  int32_t noise_mode;      /* bdl_noise_mode  */
+  int32_t collect;         /* bdl_collect     */
+  int32_t flags;           /* BDL_FLAG_*      */
+  int32_t pad0;
+  int64_t n;
+  /* scalars, already rounded from the host's float64 to fp32 exactly as torch
+   * casts a Python scalar at the op (index 0 = body group, 1 = head group). */
+  float lr[2];             /* eta                                                   */
+  float noise_scale[2];    /* csghmc: nd*sqrt(2*a*eta)/N; sghmc: nd*sqrt(2a/(N eta)); sgld: nd*sqrt(2/(N eta)) */
+  float one_minus_alpha;   /* fl32(1 - momentum_decay)                             */
+  float prior_sig;         /* csghmc: the sigma multiplying theta (quirk Q1)        */
+  float sigma2;            /* sghmc/sgld: fl32(prior_sig**2)                        */
+  float n_data;            /* fl32(ND * Ninflate)                                   */
+  float mu;                /* SGD momentum                                          */
+  float collect_a;         /* WELFORD: n; MEAN: multiplier of the old moment        */
+  float collect_b;         /* MEAN: divisor                                          */
+  float pad1;
+  uint64_t seed;           /* Philox key                                            */
+  uint64_t chain;          /* chain id (rank)                                        */
+  uint64_t step;           /* global step counter                                    */
+} bdl_step_args;
+
+/* Stand-alone posterior-moment update (no parameter update). */
+typedef struct bdl_moments_args {
+  const float* theta;
+  float* mom1;
+  float* mom2;             /* may be null */
+  int64_t n;
+  int32_t collect;         /* bdl_collect */
+  int32_t flags;           /* BDL_FLAG_RECIP_DIV */
+  float collect_a;
+  float collect_b;
+} bdl_moments_args;
+
+/* Variance form used by bdl_posterior_sample. */
+typedef enum bdl_var_mode {
+  BDL_VAR_GIVEN = 0,       /* mom2 already holds the variance                        */
+  BDL_VAR_RAW_MOMENTS = 1, /* var = ratio*(m2 - m1^2)  (sgld.py:337-345, csgld.py:396-400) */
+  BDL_VAR_WELFORD = 2      /* var = M2 / ratio_div      (csghmc.py:451-459)           */
+} bdl_var_mode;
+
+typedef struct bdl_sample_args {
+  float* out;              /* theta sample                                            */
+  const float* mom1;       /* posterior mean                                          */
+  const float* mom2;       /* variance source (see var_mode)                          */
+  const float* noise;      /* eps buffer (BDL_NOISE_BUFFER) or null (Philox)          */
+  int64_t n;
+  int32_t var_mode;
+  int32_t noise_mode;      /* BDL_NOISE_BUFFER or BDL_NOISE_PHILOX                    */
+  float ratio;             /* RAW_MOMENTS multiplier / WELFORD divisor                */
+  float var_floor;         /* clamp_(min=...) — 1e-12 in the reference                 */
+  uint64_t seed, chain, step;
+} bdl_sample_args;
+
+int bdl_version(void);
+const char* bdl_last_error(void);
+
+/* Host-only: merge segments into runs. out_runs must hold >= nseg+1 entries
+ * (gaps between segments become BDL_ATTR_SKIP runs). Returns the run count
+ * (>= 0) or a negative bdl_status. */
+int bdl_build_runs(const bdl_segment* segs, int32_t nseg, int64_t n,
+                   bdl_run* out_runs, int32_t max_runs);
+
+/* One fused SG-MCMC step (update + optional noise + optional moment collect). */
+int bdl_sgmcmc_step(const bdl_step_args* args, void* hip_stream);
+
+/* Stand-alone moment update. */
+int bdl_moments_update(const bdl_moments_args* args, void* hip_stream);
+
+/* theta_s = mean + sqrt(clamp(var)) * eps. */
+int bdl_posterior_sample(const bdl_sample_args* args, void* hip_stream);
+
+/* out[i] = the N(0,1) value the step kernel would draw for element i. */
+int bdl_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t chain,
+                      uint64_t step, void* hip_stream);
+
+/* Launch geometry override for tuning (0 = default). Returns the previous
+ * value packed as (blocks_per_cu << 16) | unroll. Not thread-safe; test only. */
+int bdl_set_launch_config(int32_t blocks_per_cu, int32_t unroll);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BDL_SGMCMC_H */

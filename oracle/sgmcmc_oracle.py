@@ -1,0 +1,353 @@
+"""ORACLE — test infrastructure, NOT product code.
+
+CPU restatement of the reference's SG-MCMC step loop (omarezz46/BayesDLL,
+methods/{csghmc,sghmc,csgld,sgld}.py + methods/cyclical.py + the
+torch.optim.SGD step they call), written op-for-op in torch-CPU fp32 so that
+every rounding happens exactly where the reference's does.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker / the timed CPU baseline — never as the
+thing measured or shipped.  The product path (bayesdll_amd) must never route
+through here.
+
+Parity pinning: tests/test_oracle_golden.py checks this restatement
+BIT-EXACTLY against golden fixtures produced by running the reference's own
+Runner/Model code (tests/golden/gen_golden.py, run in the build container where
+/root/reference is importable).
+
+The restated algorithm, with reference citations:
+  * CyclicalSchedule  — methods/cyclical.py:29-74 (int cycle length for the lr,
+    float cycle length for should_sample / last_in_cycle / cycle number: Q3).
+  * csghmc_update     — methods/csghmc.py:747-778 (grad_U = g + prior_sig*theta
+    on both branches: Q1; noise drawn every step, added only on sample steps).
+  * sghmc_model       — methods/sghmc.py:482-510 (v' = v(1-a) + lr*gU + noise;
+    p.grad = g + v').
+  * sgld_model        — methods/sgld.py:469-484 (== methods/csgld.py:665-680).
+  * sgd_step          — torch.optim.SGD single-tensor path (buf = clone(grad) on
+    the first step, else buf = mu*buf + grad; param.add_(buf, alpha=-lr)): the
+    step the reference calls at methods/sgld.py:226, sghmc.py:229, csgld.py:253.
+  * simulate_*        — the Runner loops: csghmc.py:246-384 (Welford with the
+    doubled samples_per_cycle increment, Q2, :333-348), csgld.py:195-331,
+    sgld.py:69-107 + :193-250, sghmc.py:69-110 + :196-251.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+
+# ----------------------------------------------------------------------------
+# Cyclical schedule (methods/cyclical.py)
+# ----------------------------------------------------------------------------
+class CyclicalSchedule:
+    def __init__(self, base_lr, nbr_of_cycles, epochs, proportion_exploration=0.5):
+        self.base_lr = base_lr
+        self.M = nbr_of_cycles
+        self.epochs = epochs
+        self.beta = proportion_exploration
+        self.current_epoch = 0
+
+    def _k(self, epoch, batch, bpe):
+        return epoch * bpe + batch + 1
+
+    def calculate_lr(self, epoch, batch, bpe):  # cyclical.py:29-45 (both branches equal)
+        K = self.epochs * bpe
+        L = K // self.M
+        k = self._k(epoch, batch, bpe)
+        pos = ((k - 1) % L) / L
+        return self.base_lr * (1 + np.cos(pos * np.pi)) / 2
+
+    def should_sample(self, epoch, batch, bpe):  # cyclical.py:48-59
+        L = self.epochs * bpe / self.M
+        pos = ((self._k(epoch, batch, bpe) - 1) % L) / L
+        return pos >= self.beta
+
+    def last_in_cycle(self, epoch, batch, bpe):  # cyclical.py:61-67
+        L = self.epochs * bpe / self.M
+        return (self._k(epoch, batch, bpe) % L) == 0
+
+    def get_cycle_number(self, epoch, batch, bpe):  # cyclical.py:69-74
+        L = self.epochs * bpe / self.M
+        return int((self._k(epoch, batch, bpe) - 1) // L) + 1
+
+
+# ----------------------------------------------------------------------------
+# Per-tensor update rules (torch CPU fp32, reference op order)
+# ----------------------------------------------------------------------------
+def _lr_for(name, readout, lr_body, lr_head):
+    return lr_head if readout in name else lr_body
+
+
+def csghmc_update(params, grads, moms, names, readout, lrs, prior_sig, momentum_decay, N, nd,
+                  should_sample, noise):
+    """methods/csghmc.py:747-778. Updates params in place; returns new moms."""
+    lr_body, lr_head = (lrs[0], lrs[0]) if len(lrs) == 1 else (lrs[0], lrs[1])
+    new_moms = []
+    for p, g, v, name, eps in zip(params, grads, moms, names, noise):
+        lr = _lr_for(name, readout, lr_body, lr_head)
+        grad_u = g + prior_sig * p  # Q1: identical for biases
+        ns = nd * np.sqrt((2 * momentum_decay * lr)) / N
+        nz = ns * eps
+        if should_sample:
+            v = v * (1 - momentum_decay) - lr * grad_u + nz
+        else:
+            v = v * (1 - momentum_decay) - lr * grad_u
+        new_moms.append(v)
+        p.add_(v)
+    return new_moms
+
+
+def sghmc_model(params, params0, grads, moms, names, readout, lrs, prior_sig, bias,
+                momentum_decay, N, nd, noise):
+    """methods/sghmc.py:482-510. Returns (new_grads, new_moms)."""
+    lr_body, lr_head = (lrs[0], lrs[0]) if len(lrs) == 1 else (lrs[0], lrs[1])
+    new_g, new_v = [], []
+    for p, p0, g, v, name, eps in zip(params, params0, grads, moms, names, noise):
+        lr = _lr_for(name, readout, lr_body, lr_head)
+        if "bias" in name and bias == "uninformative":
+            grad_u = g
+        else:
+            grad_u = g + (p - p0) / (prior_sig ** 2) / N
+        ns = nd * np.sqrt(2 * momentum_decay / (N * lr))
+        v = v * (1 - momentum_decay) + lr * grad_u + ns * eps
+        new_v.append(v)
+        new_g.append(g + v.clone())
+    return new_g, new_v
+
+
+def sgld_model(params, params0, grads, names, readout, lrs, prior_sig, bias, N, nd, noise):
+    """methods/sgld.py:469-484 (identical to methods/csgld.py:665-680)."""
+    lr_body, lr_head = (lrs[0], lrs[0]) if len(lrs) == 1 else (lrs[0], lrs[1])
+    out = []
+    for p, p0, g, name, eps in zip(params, params0, grads, names, noise):
+        lr = _lr_for(name, readout, lr_body, lr_head)
+        if "bias" in name and bias == "uninformative":
+            out.append(g + (nd * np.sqrt(2 / (N * lr)) * eps))
+        else:
+            out.append(g + ((p - p0) / (prior_sig ** 2) / N + nd * np.sqrt(2 / (N * lr)) * eps))
+    return out
+
+
+def sgd_step(params, grads, bufs, lrs_per_param, momentum):
+    """torch.optim.SGD (weight_decay 0, dampening 0, no nesterov), single-tensor."""
+    new_bufs = []
+    for p, g, buf, lr in zip(params, grads, bufs, lrs_per_param):
+        d = g
+        if momentum != 0:
+            if buf is None:
+                buf = torch.clone(g).detach()
+            else:
+                buf.mul_(momentum).add_(g, alpha=1)
+            d = buf
+        new_bufs.append(buf)
+        p.add_(d, alpha=-lr)
+    return new_bufs
+
+
+def posterior_variance_raw(mom1, mom2, cnt):
+    """methods/sgld.py:337-345: ratio*(m2 - m1^2) clamped at 1e-12."""
+    ratio = cnt / (cnt - 1) if cnt > 1 else 1.0
+    v = ratio * (mom2 - mom1 ** 2)
+    return v.clamp_(min=1e-12)
+
+
+def posterior_variance_welford(m2, n_samples, like):
+    """methods/csghmc.py:451-459."""
+    if n_samples > 1:
+        v = m2 / (n_samples - 1)
+    else:
+        v = torch.ones_like(like) * 1e-12
+    return v.clamp_(min=1e-12)
+
+
+def posterior_sample(mean, var, eps):
+    """methods/sgld.py:295: p_m + p_v.sqrt()*eps."""
+    return mean + var.sqrt() * eps
+
+
+# ----------------------------------------------------------------------------
+# Runner-loop simulators (drive the rules above exactly as the Runners do)
+# ----------------------------------------------------------------------------
+def _split(vec, shapes):
+    out, off = [], 0
+    for s in shapes:
+        k = int(np.prod(s))
+        out.append(torch.from_numpy(np.ascontiguousarray(vec[off:off + k])).clone().reshape(s))
+        off += k
+    return out
+
+
+def _cat(ts):
+    return torch.cat([t.reshape(-1) for t in ts]).numpy().copy()
+
+
+def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
+    """Run the reference Runner loop for cfg['method'] on prescribed grads/noise.
+
+    grad_fn(t) -> flat np.float32 gradient of step t; noise_fn(t) -> flat
+    np.float32 standard-normal draws of step t (named_parameters order).
+    Returns a dict shaped like the golden fixtures.
+    """
+    method = cfg["method"]
+    hp = {k: str(v) for k, v in cfg["hparams"].items()}
+    names = [nm for nm, _ in segments]
+    shapes = [tuple(s) for _, s in segments]
+    params = _split(theta_init, shapes)
+    params0 = _split(prior_mean, shapes)
+    N = cfg["ND"] * float(hp["Ninflate"])
+    nd = float(hp["nd"])
+    prior_sig = float(hp["prior_sig"])
+    bias = str(hp["bias"])
+    thin = int(hp["thin"])
+    nst = int(hp["nst"])
+    lr0, lr_head0 = cfg["lr"], cfg["lr_head"]
+    bpe, epochs = cfg["bpe"], cfg["epochs"]
+    is_head = [readout in nm for nm in names]
+
+    rec = dict(lrs=[], should_sample=[], theta=[], mom=[])
+    step = 0
+
+    def grads_now(t):
+        return _split(grad_fn(t), shapes)
+
+    def noise_now(t):
+        return _split(noise_fn(t), shapes)
+
+    if method in ("csghmc", "csgld"):
+        sched = CyclicalSchedule(lr0, cfg.get("num_cycles", 10), epochs, cfg.get("beta", 0.5))
+        alpha = float(hp.get("momentum_decay", 0.0))
+        moms = [torch.zeros_like(p) for p in params]  # csghmc momentum
+        bufs = [None] * len(params)                    # csgld SGD buffers
+        m1, m2, spc = {}, {}, {}
+        samples_collected, current_cycle = 0, 0
+        for ep in range(epochs):
+            for b in range(bpe):
+                lr = sched.calculate_lr(ep, b, bpe)
+                ss = sched.should_sample(ep, b, bpe) and b % thin == 0
+                last = sched.last_in_cycle(ep, b, bpe)
+                lrs = [lr, lr * (lr_head0 / lr0)]
+                rec["lrs"].append([float(x) for x in lrs])
+                rec["should_sample"].append(bool(ss) if method == "csghmc" else False)
+                rec["theta"].append(_cat(params))
+                g, eps = grads_now(step), noise_now(step)
+                if method == "csghmc":
+                    rec["mom"].append(_cat(moms))
+                    moms = csghmc_update(params, g, moms, names, readout, lrs, prior_sig, alpha, N,
+                                         nd, ss, eps)
+                else:
+                    rec["mom"].append(_cat([torch.zeros_like(p) if bb is None else bb
+                                            for p, bb in zip(params, bufs)]))
+                    newg = sgld_model(params, params0, g, names, readout, lrs, prior_sig, bias, N,
+                                      nd, eps)
+                    bufs = sgd_step(params, newg, bufs, [lrs[1] if h else lrs[0] for h in is_head],
+                                    cfg.get("momentum", 0.0))
+                step += 1
+                if ss:
+                    c = sched.get_cycle_number(ep, b, bpe)
+                    tv = torch.cat([p.reshape(-1) for p in params])
+                    if method == "csghmc":  # Welford, csghmc.py:333-348 (Q2)
+                        if c not in m1:
+                            m1[c] = tv.clone()
+                            m2[c] = torch.zeros_like(tv)
+                            spc[c] = 1
+                        else:
+                            nn_ = spc.get(c, 0) + 1
+                            delta = tv - m1[c]
+                            m1[c] += delta / nn_
+                            delta2 = tv - m1[c]
+                            m2[c] += delta * delta2
+                            spc[c] = nn_
+                    else:  # csgld.py:280-293
+                        if c not in m1:
+                            m1[c] = tv.clone()
+                            m2[c] = tv ** 2
+                        else:
+                            cc = spc.get(c, 0) + 1
+                            m1[c] = (tv + (cc - 1) * m1[c]) / cc
+                            m2[c] = (tv ** 2 + (cc - 1) * m2[c]) / cc
+                    samples_collected += 1
+                    spc[c] = spc.get(c, 0) + 1
+                if last:
+                    c = sched.get_cycle_number(ep, b, bpe)
+                    if c > current_cycle:
+                        current_cycle = c
+        rec["theta"].append(_cat(params))
+        rec["mom"].append(_cat(moms) if method == "csghmc" else
+                          _cat([torch.zeros_like(p) if bb is None else bb
+                                for p, bb in zip(params, bufs)]))
+        cycles = sorted(m1.keys())
+        out = {k: np.array(v) for k, v in rec.items()}
+        out["cycles"] = np.array(cycles, np.int64)
+        out["cycle_mom1"] = np.stack([m1[c].numpy() for c in cycles]) if cycles else None
+        out["cycle_mom2"] = np.stack([m2[c].numpy() for c in cycles]) if cycles else None
+        out["samples_per_cycle"] = np.array([spc[c] for c in cycles], np.int64)
+        out["samples_collected"] = samples_collected
+        out["current_cycle"] = current_cycle
+        return out
+
+    # sgld / sghmc: burn-in, then running moments every `thin` global iterations
+    burnin = int(hp["burnin"])
+    momentum = cfg.get("momentum", 0.0) if method == "sgld" else 0.0
+    alpha = float(hp.get("momentum_decay", 0.0))
+    moms = [torch.zeros_like(p) for p in params]
+    bufs = [None] * len(params)
+    lrs = [lr0, lr_head0]
+    lr_per_param = [lr_head0 if h else lr0 for h in is_head]
+    bi = 0
+    m1 = m2 = None
+    cnt = 0
+    for ep in range(epochs):
+        if ep == burnin:  # sgld.py:95-102
+            tv = torch.cat([p.reshape(-1) for p in params])
+            m1 = tv * 1.0
+            if nst > 0:
+                m2 = tv ** 2
+            cnt = 1
+        collect = ep >= burnin
+        for b in range(bpe):
+            rec["lrs"].append([float(x) for x in lrs])
+            rec["should_sample"].append(False)
+            rec["theta"].append(_cat(params))
+            g, eps = grads_now(step), noise_now(step)
+            if method == "sghmc":
+                rec["mom"].append(_cat(moms))
+                newg, moms = sghmc_model(params, params0, g, moms, names, readout, lrs, prior_sig,
+                                         bias, alpha, N, nd, eps)
+            else:
+                rec["mom"].append(_cat([torch.zeros_like(p) if bb is None else bb
+                                        for p, bb in zip(params, bufs)]))
+                newg = sgld_model(params, params0, g, names, readout, lrs, prior_sig, bias, N, nd,
+                                  eps)
+            bufs = sgd_step(params, newg, bufs, lr_per_param, momentum)
+            step += 1
+            bi += 1
+            if collect and bi % thin == 0:  # sgld.py:239-246
+                tv = torch.cat([p.reshape(-1) for p in params])
+                m1 = (tv + cnt * m1) / (cnt + 1)
+                if nst > 0:
+                    m2 = (tv ** 2 + cnt * m2) / (cnt + 1)
+                cnt += 1
+    rec["theta"].append(_cat(params))
+    rec["mom"].append(_cat(moms) if method == "sghmc" else
+                      _cat([torch.zeros_like(p) if bb is None else bb
+                            for p, bb in zip(params, bufs)]))
+    out = {k: np.array(v) for k, v in rec.items()}
+    out["post_mom1"] = m1.numpy()
+    out["post_mom2"] = m2.numpy() if m2 is not None else np.zeros(0, np.float32)
+    out["post_cnt"] = cnt
+    return out
+
+
+def csghmc_step_cpu(params, grads, moms, names, readout, lrs, prior_sig, momentum_decay, N, nd,
+                    should_sample, generator=None):
+    """The reference csghmc per-tensor loop with its own torch.randn_like draws
+    (used as the timed CPU baseline in bench.py: the RNG is part of the step)."""
+    noise = [torch.randn(p.shape, generator=generator) if generator is not None
+             else torch.randn_like(p) for p in params]
+    return csghmc_update(params, grads, moms, names, readout, lrs, prior_sig, momentum_decay, N,
+                         nd, should_sample, noise)
+
+
+__all__ = ["CyclicalSchedule", "csghmc_update", "sghmc_model", "sgld_model", "sgd_step",
+           "posterior_variance_raw", "posterior_variance_welford", "posterior_sample", "simulate",
+           "csghmc_step_cpu"]

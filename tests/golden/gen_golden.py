@@ -1,0 +1,282 @@
+"""Generate the golden fixtures from the REFERENCE sampler (container-only tool).
+
+Runs the reference's own Runner/Model code (methods/{csghmc,csgld,sgld,sghmc}.py,
+methods/cyclical.py) imported read-only from /root/reference, on a FakeNet whose
+backward returns prescribed gradients (tests/fakenet.py), and records:
+
+  * per step: the lrs handed to Model.forward, should_sample (csghmc), and every
+    torch.randn_like draw made inside Model.forward (one per tensor per step,
+    named_parameters order: methods/csghmc.py:766, methods/sgld.py:478/483,
+    methods/sghmc.py:501), captured by wrapping torch.randn_like;
+  * theta and the momentum / SGD buffer before every step and after the last;
+  * the final posterior moments, counts and per-cycle dictionaries;
+  * cyclical schedule tables (methods/cyclical.py:29-74) for several configs,
+    including K % M != 0 (quirk Q3).
+
+Usage (in the build container, where /root/reference exists):
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+The outputs are the small .npz files next to this script; the reference
+itself never leaves the container.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import logging
+import os
+import sys
+import tempfile
+import types
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))  # tests/ for fakenet
+from fakenet import (TOY_SEGMENTS, TOY_READOUT, FakeNet, fake_loader, init_vector,  # noqa: E402
+                     numel_of)
+
+REF = "/root/reference"
+
+
+def import_reference():
+    tv = types.ModuleType("torchvision")
+    for sub in ["transforms", "models", "datasets"]:
+        m = types.ModuleType("torchvision." + sub)
+        setattr(tv, sub, m)
+        sys.modules["torchvision." + sub] = m
+    sys.modules["torchvision"] = tv
+    sys.path[:0] = [REF, os.path.join(REF, "src")]
+    import methods.csghmc
+    import methods.csgld
+    import methods.cyclical
+    import methods.sghmc
+    import methods.sgld
+    return methods
+
+
+class Capture:
+    """Wrap torch.randn_like; record draws made while `active`."""
+
+    def __init__(self):
+        self.active = False
+        self.draws = []
+        self._orig = torch.randn_like
+
+    def __enter__(self):
+        orig = self._orig
+
+        def wrapped(t, *a, **k):
+            out = orig(t, *a, **k)
+            if self.active:
+                self.draws.append(out.detach().clone().reshape(-1))
+            return out
+
+        torch.randn_like = wrapped
+        return self
+
+    def __exit__(self, *exc):
+        torch.randn_like = self._orig
+
+
+def flat(params):
+    return torch.nn.utils.parameters_to_vector([p.detach() for p in params]).numpy().copy()
+
+
+def make_args(tmp, **kw):
+    a = dict(device="cpu", ND=50, pretrained=None, lr=0.05, lr_head=0.1, momentum=0.5, epochs=4,
+             num_cycles=2, proportion_exploration=0.5, full_sample=False, test_eval_freq=1,
+             ece_num_bins=15, log_dir=tmp, num_classes=10)
+    a.update(kw)
+    return SimpleNamespace(**a)
+
+
+def run_method(methods, method, cfg):
+    """Drive one reference Runner for cfg['epochs'] epochs; return the record."""
+    torch.manual_seed(cfg["torch_seed"])
+    n = numel_of(TOY_SEGMENTS)
+    theta_init = init_vector(cfg["init_seed"], n, cfg["init_scale"])
+    net = FakeNet(grad_seed=cfg["grad_seed"], grad_scale=cfg["grad_scale"], init=theta_init)
+    net0 = None
+    prior = np.zeros(n, np.float32)
+    if cfg.get("prior_seed") is not None:
+        prior = init_vector(cfg["prior_seed"], n, 0.3)
+        net0 = FakeNet(init=prior)
+    tmp = tempfile.mkdtemp(prefix="bdl_golden_")
+    args = make_args(tmp, pretrained=("fake" if net0 is not None else None), epochs=cfg["epochs"],
+                     num_cycles=cfg.get("num_cycles", 2), lr=cfg["lr"], lr_head=cfg["lr_head"],
+                     momentum=cfg.get("momentum", 0.0), ND=cfg["ND"],
+                     proportion_exploration=cfg.get("beta", 0.5),
+                     hparams={k: str(v) for k, v in cfg["hparams"].items()})
+    logger = logging.getLogger("golden")
+    mod = getattr(methods, method)
+    runner = mod.Runner(net, net0, args, logger)
+    model_cls = mod.Model
+
+    rec = dict(lrs=[], should_sample=[], theta=[], mom=[], noise=[])
+    cap = Capture()
+    orig_forward = model_cls.forward
+
+    def state_mom():
+        if method in ("csghmc", "sghmc"):
+            if not hasattr(runner.model, "momentum_buffer"):
+                return np.zeros(n, np.float32)
+            return torch.cat([runner.model.momentum_buffer[nm].reshape(-1)
+                              for nm, _ in runner.net.named_parameters()]).numpy().copy()
+        bufs = []
+        for p in runner.net.parameters():
+            st = runner.optimizer.state.get(p, {})
+            b = st.get("momentum_buffer")
+            bufs.append(np.zeros(p.numel(), np.float32) if b is None else b.reshape(-1).numpy())
+        return np.concatenate(bufs).astype(np.float32)
+
+    def fwd(self, x, y, net_, net0_, criterion, lrs, Ninflate=1.0, nd=1.0, **kw):
+        rec["lrs"].append([float(v) for v in lrs])
+        rec["should_sample"].append(bool(kw.get("should_sample", False)))
+        rec["theta"].append(flat(runner.net.parameters()))
+        rec["mom"].append(state_mom())
+        cap.active, cap.draws = True, []
+        try:
+            return orig_forward(self, x, y, net_, net0_, criterion, lrs, Ninflate, nd, **kw)
+        finally:
+            cap.active = False
+            rec["noise"].append(torch.cat(cap.draws).numpy().copy())
+
+    model_cls.forward = fwd
+    try:
+        with cap:
+            loader = fake_loader(cfg["bpe"])
+            if method in ("csghmc", "csgld"):
+                for ep in range(cfg["epochs"]):
+                    runner.cyclical_scheduler.current_epoch = ep
+                    runner.train_one_epoch(loader)
+            else:  # sgld / sghmc: Runner.train's epoch loop minus evaluation
+                bi = 0
+                for ep in range(cfg["epochs"]):
+                    if ep == runner.burnin:
+                        with torch.no_grad():
+                            tv = torch.nn.utils.parameters_to_vector(runner.net.parameters())
+                            runner.post_theta_mom1 = tv * 1.0
+                            if runner.nst > 0:
+                                runner.post_theta_mom2 = tv ** 2
+                        runner.post_theta_cnt = 1
+                    _, _, bi = runner.train_one_epoch(loader, collect=(ep >= runner.burnin), bi=bi)
+    finally:
+        model_cls.forward = orig_forward
+
+    out = dict(
+        config=json.dumps(dict(cfg, method=method)),
+        segments=json.dumps([[nm, list(s)] for nm, s in TOY_SEGMENTS]),
+        readout=TOY_READOUT,
+        theta_init=theta_init,
+        prior_mean=prior,
+        lrs=np.array(rec["lrs"], np.float64),
+        should_sample=np.array(rec["should_sample"], bool),
+        noise=np.stack(rec["noise"]).astype(np.float32),
+        theta=np.stack(rec["theta"] + [flat(runner.net.parameters())]).astype(np.float32),
+    )
+    rec["mom"].append(state_mom())
+    out["mom"] = np.stack(rec["mom"]).astype(np.float32)
+    if method in ("csghmc", "csgld"):
+        cycles = sorted(runner.cycle_theta_mom1.keys())
+        out["cycles"] = np.array(cycles, np.int64)
+        out["cycle_mom1"] = np.stack([runner.cycle_theta_mom1[c].numpy() for c in cycles]) \
+            if cycles else np.zeros((0, n), np.float32)
+        out["cycle_mom2"] = np.stack([runner.cycle_theta_mom2[c].numpy() for c in cycles]) \
+            if cycles else np.zeros((0, n), np.float32)
+        out["samples_per_cycle"] = np.array([runner.samples_per_cycle[c] for c in cycles], np.int64)
+        out["samples_collected"] = np.int64(runner.samples_collected)
+        out["current_cycle"] = np.int64(runner.current_cycle)
+        out["ckpt_files"] = np.array(sorted(os.listdir(tmp)))
+    else:
+        out["post_mom1"] = runner.post_theta_mom1.numpy()
+        out["post_mom2"] = runner.post_theta_mom2.numpy() if runner.nst > 0 else np.zeros(0, np.float32)
+        out["post_cnt"] = np.int64(runner.post_theta_cnt)
+    return out
+
+
+CONFIGS = {
+    # cSGHMC (config 2 hyper-parameters, scaled to make every term visible)
+    "csghmc_k20": ("csghmc", dict(epochs=4, bpe=5, num_cycles=2, beta=0.5, lr=0.05, lr_head=0.1,
+                                  ND=50, torch_seed=7, init_seed=11, init_scale=0.5, grad_seed=101,
+                                  grad_scale=0.5,
+                                  hparams=dict(prior_sig=0.7, bias="informative",
+                                               momentum_decay=0.18, Ninflate=1.0, nd=1.0,
+                                               burnin=0, thin=2, nst=2))),
+    # K % M != 0: lr restarts and cycle numbers drift apart, last_in_cycle never fires (Q3)
+    "csghmc_k21": ("csghmc", dict(epochs=3, bpe=7, num_cycles=2, beta=0.5, lr=0.05, lr_head=0.2,
+                                  ND=40, torch_seed=8, init_seed=12, init_scale=0.5, grad_seed=102,
+                                  grad_scale=0.3,
+                                  hparams=dict(prior_sig=1.0, bias="uninformative",
+                                               momentum_decay=0.3, Ninflate=2.0, nd=0.5,
+                                               burnin=0, thin=1, nst=2))),
+    "csgld_k20": ("csgld", dict(epochs=4, bpe=5, num_cycles=2, beta=0.5, lr=0.05, lr_head=0.1,
+                                momentum=0.5, ND=50, torch_seed=9, init_seed=13, init_scale=0.5,
+                                grad_seed=103, grad_scale=0.5,
+                                hparams=dict(prior_sig=0.7, bias="informative", Ninflate=1.0,
+                                             nd=1.0, nst=2, thin=2))),
+    "sgld_inf": ("sgld", dict(epochs=3, bpe=5, lr=0.05, lr_head=0.1, momentum=0.5, ND=50,
+                              torch_seed=10, init_seed=14, init_scale=0.5, grad_seed=104,
+                              grad_scale=0.5, prior_seed=21,
+                              hparams=dict(prior_sig=0.8, bias="informative", Ninflate=1.0,
+                                           nd=1.0, burnin=1, thin=2, nst=2))),
+    "sgld_uninf_nomom": ("sgld", dict(epochs=3, bpe=5, lr=0.02, lr_head=0.05, momentum=0.0,
+                                      ND=30, torch_seed=11, init_seed=15, init_scale=0.5,
+                                      grad_seed=105, grad_scale=0.5, prior_seed=22,
+                                      hparams=dict(prior_sig=0.5, bias="uninformative",
+                                                   Ninflate=10.0, nd=0.1, burnin=1, thin=3,
+                                                   nst=0))),
+    "sghmc_inf": ("sghmc", dict(epochs=3, bpe=5, lr=0.05, lr_head=0.1, ND=50, torch_seed=12,
+                                init_seed=16, init_scale=0.5, grad_seed=106, grad_scale=0.5,
+                                prior_seed=23,
+                                hparams=dict(prior_sig=0.8, bias="informative",
+                                             momentum_decay=0.18, Ninflate=1.0, nd=1.0,
+                                             burnin=1, thin=2, nst=2))),
+    "sghmc_uninf": ("sghmc", dict(epochs=3, bpe=4, lr=0.02, lr_head=0.04, ND=30, torch_seed=13,
+                                  init_seed=17, init_scale=0.5, grad_seed=107, grad_scale=0.5,
+                                  prior_seed=24,
+                                  hparams=dict(prior_sig=1.5, bias="uninformative",
+                                               momentum_decay=0.3, Ninflate=5.0, nd=0.2,
+                                               burnin=1, thin=2, nst=2))),
+}
+
+SCHEDULES = [(4, 5, 2, 0.5), (3, 7, 2, 0.5), (10, 7, 3, 0.3), (7, 10, 3, 0.5), (5, 3, 4, 0.25),
+             (2, 115, 4, 0.5)]
+
+
+def schedule_tables(methods):
+    C = methods.cyclical.CyclicalSGMCMC
+    out = {}
+    for (E, B, M, beta) in SCHEDULES:
+        s = C(base_lr=0.1, nbr_of_cycles=M, epochs=E, proportion_exploration=beta)
+        rows = []
+        for ep in range(E):
+            for b in range(B):
+                rows.append((float(s.calculate_lr(ep, b, B)), bool(s.should_sample(ep, b, B)),
+                             bool(s.last_in_cycle(ep, b, B)), int(s.get_cycle_number(ep, b, B))))
+        key = f"E{E}_B{B}_M{M}_beta{beta}"
+        out[key + "_lr"] = np.array([r[0] for r in rows], np.float64)
+        out[key + "_sample"] = np.array([r[1] for r in rows], bool)
+        out[key + "_last"] = np.array([r[2] for r in rows], bool)
+        out[key + "_cycle"] = np.array([r[3] for r in rows], np.int64)
+    out["configs"] = json.dumps(SCHEDULES)
+    return out
+
+
+def main():
+    os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
+    logging.basicConfig(level=logging.WARNING)
+    methods = import_reference()
+    torch.set_num_threads(1)
+    for name, (method, cfg) in CONFIGS.items():
+        rec = run_method(methods, method, copy.deepcopy(cfg))
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **rec)
+        print(f"wrote {path}: steps={rec['lrs'].shape[0]} n={rec['theta'].shape[1]}")
+    np.savez_compressed(os.path.join(HERE, "schedule.npz"), **schedule_tables(methods))
+    print("wrote schedule.npz")
+
+
+if __name__ == "__main__":
+    main()
