@@ -1,0 +1,214 @@
+"""Runner pieces shared by the four drop-in samplers (host-side, off the hot path).
+
+Mirrors the reference Runners' evaluation / bookkeeping API
+(methods/csghmc.py:211-244, :387-670; methods/sgld.py:253-398) on top of the
+flat device buffers:
+
+  * posterior draws go through ONE fused kernel per draw (bdl_posterior_sample:
+    theta_s = mean + sqrt(clamp(var)) * eps over the whole flat vector) written
+    straight into the flat parameter buffer of an evaluation copy of the net,
+    instead of nst x tensors-many torch ops (methods/sgld.py:292-296);
+  * with several chains (torch.distributed initialised, one chain per GPU),
+    the posterior-predictive average is one all_reduce(SUM) of per-chain
+    predictive probabilities over RCCL — the only collective in the design.
+"""
+from __future__ import annotations
+
+import copy
+import os
+import pickle
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import _lib as L
+from . import kernels as K
+from .flat import bind_parameters, fill_normal_per_tensor
+
+EVAL_STEP_BASE = 1 << 62  # Philox step keys for evaluation draws (never used by training)
+
+
+class PosteriorDraw:
+    """An evaluation copy of `net` whose flat theta the sample kernel fills."""
+
+    def __init__(self, net, noise_mode, seed, chain):
+        self.net = copy.deepcopy(net)
+        for p in self.net.parameters():
+            p.grad = None
+        self.theta = bind_parameters(self.net)
+        self.numels = [p.numel() for p in self.net.parameters()]
+        self.noise_mode = noise_mode
+        self.seed = seed
+        self.chain = chain
+        self.count = 0
+        self.noise = None if noise_mode == "philox" else torch.empty_like(self.theta)
+
+    def load_mean(self, mean):
+        self.theta.copy_(mean)
+
+    def draw(self, mean, m2, var_mode, ratio):
+        """theta = mean + sqrt(clamp(var, 1e-12)) * eps; m2=None -> var = 1e-12."""
+        noise = None
+        if self.noise_mode != "philox":
+            noise = fill_normal_per_tensor(self.noise, self.numels)
+        K.posterior_sample(self.theta, mean, m2, var_mode=var_mode, ratio=ratio, noise=noise,
+                           seed=self.seed, chain=self.chain, step=EVAL_STEP_BASE + self.count)
+        self.count += 1
+
+
+def chain_world():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size()
+    return 1
+
+
+def chain_average_logprob(logp):
+    """log of the across-chain mean predictive probability (one RCCL all_reduce).
+
+    Per chain, logp = log p_chain(y|x) ([B, C]); returns log((1/K) sum_k p_k),
+    the multi-chain analogue of logsumexp(...) - log(nst) (methods/sgld.py:300).
+    """
+    import torch.distributed as dist
+    k = chain_world()
+    if k == 1:
+        return logp
+    p = logp.exp()
+    dist.all_reduce(p, op=dist.ReduceOp.SUM)
+    return (p / k).log()
+
+
+def evaluate_point_estimate(runner, data_loader, net_to_evaluate):
+    """methods/csghmc.py:211-244."""
+    args = runner.args
+    net_to_evaluate.eval()
+    loss, error, nb = 0.0, 0, 0
+    with torch.no_grad():
+        for x, y in data_loader:
+            x, y = x.to(args.device), y.to(args.device)
+            out = net_to_evaluate(x)
+            lb = runner.criterion(out, y)
+            pred = out.data.max(dim=1)[1]
+            loss += lb.item() * len(y)
+            error += pred.ne(y.data).sum().item()
+            nb += len(y)
+    if nb == 0:
+        return 0.0, 0.0
+    return loss / nb, error / nb
+
+
+def save_logits(args, targets, logits, logits_all, suffix=None):
+    suffix = "" if suffix is None else f"_{suffix}"
+    fname = os.path.join(args.log_dir, f"logits{suffix}.pkl")
+    with open(fname, "wb") as ff:
+        pickle.dump({"targets": targets, "logits": logits, "logits_all": logits_all}, ff,
+                    protocol=pickle.HIGHEST_PROTOCOL)
+    return fname
+
+
+def gmm_weights(cycle_likelihoods):
+    """methods/csghmc.py:641-670: w_c = 1 / mean(1/lik), normalised."""
+    if not cycle_likelihoods:
+        return {0: 1.0}
+    w = {c: 1.0 / np.mean([1.0 / lk for lk in liks]) for c, liks in cycle_likelihoods.items()}
+    tot = sum(w.values())
+    if tot > 0:
+        return {c: v / tot for c, v in w.items()}
+    return {c: 1.0 / len(w) for c in w}
+
+
+def mixture_evaluate(runner, test_loader, var_of_cycle):
+    """Cyclical methods' GMM predictive (methods/csghmc.py:387-514,
+    methods/csgld.py:337-452).  var_of_cycle(c) -> (m2, var_mode, ratio)."""
+    args = runner.args
+    weights = runner.calculate_gmm_weights()
+    runner.logger.info(f"GMM component weights: {weights}")
+    model = runner.model
+    draw = PosteriorDraw(runner.net, model.noise_mode, model.seed, model.chain)
+    loss, error, nb = 0.0, 0, 0
+    targets, logits, logits_all = [], [], []
+    draw.net.eval()
+    with torch.no_grad():
+        for x, y in test_loader:
+            x, y = x.to(args.device), y.to(args.device)
+            comp_all, batch_logits = [], None
+            for cycle in runner.cycle_theta_mom1.keys():
+                weight = weights.get(cycle, 0.0)
+                if weight < 1e-10:
+                    continue
+                mean = runner.cycle_theta_mom1[cycle]
+                outs = []
+                if runner.nst == 0:
+                    draw.load_mean(mean)
+                    outs.append(draw.net(x))
+                else:
+                    m2, var_mode, ratio = var_of_cycle(cycle)
+                    for _ in range(runner.nst):
+                        draw.draw(mean, m2, var_mode, ratio)
+                        outs.append(draw.net(x))
+                comp = torch.stack(outs, dim=2)
+                if runner.nst == 0:
+                    comp_out = comp.squeeze(2)
+                else:
+                    comp_out = F.log_softmax(comp, dim=1).logsumexp(-1) - np.log(runner.nst)
+                comp_all.append(comp)
+                batch_logits = weight * comp_out if batch_logits is None else \
+                    batch_logits + weight * comp_out
+            comp_all = torch.stack(comp_all, dim=3) if comp_all else torch.zeros(
+                (x.size(0), args.num_classes, 1, 1), device=x.device)
+            if batch_logits is None:  # no cycle collected yet
+                batch_logits = draw.net(x)
+            batch_logits = chain_average_logprob(batch_logits) if chain_world() > 1 else batch_logits
+            lb = runner.criterion(batch_logits, y)
+            pred = batch_logits.data.max(dim=1)[1]
+            targets.append(y.cpu().numpy())
+            logits.append(batch_logits.cpu().numpy())
+            logits_all.append(comp_all.cpu().numpy())
+            loss += lb.item() * len(y)
+            error += pred.ne(y.data).sum().item()
+            nb += len(y)
+    return (loss / nb, error / nb, np.concatenate(targets, 0), np.concatenate(logits, 0),
+            np.concatenate(logits_all, 0))
+
+
+def sample_average_evaluate(runner, test_loader, mean, m2, var_mode, ratio):
+    """sgld/sghmc predictive: average over nst posterior draws
+    (methods/sgld.py:253-321), across chains via chain_average_logprob."""
+    args = runner.args
+    model = runner.model
+    draw = PosteriorDraw(runner.net, model.noise_mode, model.seed, model.chain)
+    draw.net.eval()
+    loss, error, nb = 0.0, 0, 0
+    targets, logits, logits_all = [], [], []
+    with torch.no_grad():
+        for x, y in test_loader:
+            x, y = x.to(args.device), y.to(args.device)
+            outs = []
+            if runner.nst == 0:
+                draw.load_mean(mean)
+                outs.append(draw.net(x))
+                la = torch.stack(outs, 2)
+                lg = F.log_softmax(la, 1).logsumexp(-1)
+            else:
+                for _ in range(runner.nst):
+                    draw.draw(mean, m2, var_mode, ratio)
+                    outs.append(draw.net(x))
+                la = torch.stack(outs, 2)
+                lg = F.log_softmax(la, 1).logsumexp(-1) - np.log(runner.nst)
+            if chain_world() > 1:
+                lg = chain_average_logprob(lg)
+            lb = runner.criterion(lg, y)
+            pred = lg.data.max(dim=1)[1]
+            targets.append(y.cpu().numpy())
+            logits.append(lg.cpu().numpy())
+            logits_all.append(la.cpu().numpy())
+            loss += lb.item() * len(y)
+            error += pred.ne(y.data).sum().item()
+            nb += len(y)
+    return (loss / nb, error / nb, np.concatenate(targets, 0), np.concatenate(logits, 0),
+            np.concatenate(logits_all, 0))
+
+
+__all__ = ["PosteriorDraw", "chain_average_logprob", "evaluate_point_estimate", "save_logits",
+           "gmm_weights", "mixture_evaluate", "sample_average_evaluate", "L"]

@@ -189,7 +189,16 @@ __device__ __forceinline__ void update_elem(const KArgs& a, uint32_t attr, float
   const float eta = head ? a.lr1 : a.lr0;
   const float ns = head ? a.ns1 : a.ns0;
 
-  if (!skip) {
+  if (!skip && (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) && (a.flags & BDL_FLAG_GRAD_READY)) {
+    // the sampler gradient was formed (and possibly clipped) by a previous
+    // *_GRAD launch: only torch.optim.SGD's step remains
+    float stepv = g;
+    if (METHOD == BDL_SGLD && (a.flags & BDL_FLAG_MOMENTUM)) {
+      v = (a.flags & BDL_FLAG_FIRST_STEP) ? g : (a.mu * v + g);
+      stepv = v;
+    }
+    th = fmaf(-eta, stepv, th);
+  } else if (!skip) {
     if constexpr (METHOD == BDL_CSGHMC) {
       // csghmc.py:759-762 — both branches are grad + prior_sig * theta (Q1)
       const float t = a.prior_sig * th;

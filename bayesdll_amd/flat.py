@@ -1,0 +1,237 @@
+"""Flat, HBM-resident state of one SG-MCMC chain.
+
+The reference keeps parameters, gradients, momenta and posterior moments as
+hundreds of separate tensors (one per named parameter) and walks them in a
+Python loop (methods/csghmc.py:747-778).  Here every per-chain quantity is ONE
+contiguous fp32 vector in the canonical `parameters_to_vector` order
+(methods/csghmc.py:328, methods/sgld.py:98), so the fused kernel sweeps each
+of them exactly once per step:
+
+    theta  — the network's parameters; every nn.Parameter's .data is rebound
+             to a view into it, so the network computes with it directly.
+    grad   — every parameter's .grad is a view into it; autograd accumulates
+             in place (the Model zeroes it instead of net.zero_grad()).
+    mom    — cSGHMC/SGHMC momentum v, or the SGD momentum buffer (sgld/csgld).
+    prior  — theta0 = net0's parameters (sgld/sghmc prior mean).
+    noise  — only in "torch" noise mode: per-tensor torch normal_ draws.
+
+The segment table (offset, numel, attributes per named parameter) is reduced
+once by the library's bdl_build_runs into a handful of runs (maximal ranges
+of equal attributes: lr group from `readout_name in pname`, prior on/off from
+`'bias' in pname and bias == 'uninformative'`, methods/sgld.py:471-479), kept
+on the device for the kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+def segment_attrs(names, readout_name, bias, requires_grad):
+    attrs = []
+    for nm, rg in zip(names, requires_grad):
+        a = 0
+        if readout_name is not None and readout_name in nm:
+            a |= L.ATTR_HEAD
+        if not ("bias" in nm and bias == "uninformative"):
+            a |= L.ATTR_PRIOR
+        if not rg:
+            a |= L.ATTR_SKIP
+        attrs.append(a)
+    return attrs
+
+
+def build_runs(offsets, numels, attrs, n):
+    """Host-side call of bdl_build_runs; returns an int64 [nruns, 2] CPU tensor."""
+    nseg = len(offsets)
+    segs = (L.Segment * max(nseg, 1))()
+    for i, (o, k, a) in enumerate(zip(offsets, numels, attrs)):
+        segs[i].offset, segs[i].numel, segs[i].attr, segs[i].pad = int(o), int(k), int(a), 0
+    cap = 2 * nseg + 2
+    runs = (L.Run * cap)()
+    nr = L.lib().bdl_build_runs(segs, nseg, int(n), runs, cap)
+    if nr < 0:
+        L.check(nr, "bdl_build_runs")
+    out = torch.empty(nr, 2, dtype=torch.int64)
+    for i in range(nr):
+        out[i, 0] = runs[i].end
+        out[i, 1] = runs[i].attr
+    return out
+
+
+class FlatState:
+    """Flat buffers for one chain, bound to `net`'s parameters and grads."""
+
+    def __init__(self, net, net0=None, *, readout_name=None, bias="informative",
+                 need_prior=False, need_mom=True, need_noise=False):
+        named = list(net.named_parameters())
+        if not named:
+            raise ValueError("bayesdll_amd: the network has no parameters")
+        self.names = [nm for nm, _ in named]
+        self.params = [p for _, p in named]
+        self.shapes = [tuple(p.shape) for p in self.params]
+        self.numels = [p.numel() for p in self.params]
+        self.offsets = np.concatenate([[0], np.cumsum(self.numels)[:-1]]).astype(np.int64).tolist()
+        self.n = int(sum(self.numels))
+        dev = self.params[0].device
+        for nm, p in named:
+            L.require_hip(p.data, f"parameter {nm!r}")
+            if p.device != dev:
+                raise RuntimeError("bayesdll_amd: all parameters must be on one device")
+        self.device = dev
+        self.readout_name = readout_name if readout_name is not None else getattr(
+            net, "readout_name", None)
+        self.bias = bias
+        self.requires_grad = [p.requires_grad for p in self.params]
+
+        # theta: copy then rebind every parameter as a view (same storage order
+        # as nn.utils.parameters_to_vector)
+        self.theta = torch.empty(self.n, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for p, o, k in zip(self.params, self.offsets, self.numels):
+                self.theta[o:o + k].copy_(p.data.reshape(-1))
+                p.data = self.theta[o:o + k].view(p.shape)
+        self.grad = torch.zeros(self.n, dtype=torch.float32, device=dev)
+        self._bind_grads()
+
+        self.mom = torch.zeros(self.n, dtype=torch.float32, device=dev) if need_mom else None
+        self.prior = None
+        if need_prior:
+            self.prior = torch.zeros(self.n, dtype=torch.float32, device=dev)
+            if net0 is not None:
+                p0 = list(net0.parameters())
+                if [tuple(q.shape) for q in p0] != self.shapes:
+                    raise ValueError("bayesdll_amd: net0 does not match net's parameter shapes")
+                with torch.no_grad():
+                    for q, o, k in zip(p0, self.offsets, self.numels):
+                        self.prior[o:o + k].copy_(q.detach().reshape(-1))
+        self.noise = torch.empty(self.n, dtype=torch.float32, device=dev) if need_noise else None
+
+        attrs = segment_attrs(self.names, self.readout_name, bias, self.requires_grad)
+        self.attrs = attrs
+        self.runs = build_runs(self.offsets, self.numels, attrs, self.n).to(dev)
+        self.nruns = int(self.runs.shape[0])
+
+    @classmethod
+    def from_segments(cls, segments, readout_name, *, bias="informative", device="cuda",
+                      need_prior=False, need_mom=True, need_noise=False, init=None):
+        """Flat chain state for a segment table alone (no nn.Module): the
+        benchmark and kernel tests use it with synthetic vectors."""
+        self = cls.__new__(cls)
+        self.names = [nm for nm, _ in segments]
+        self.shapes = [tuple(s) for _, s in segments]
+        self.numels = [int(np.prod(s)) for s in self.shapes]
+        self.offsets = np.concatenate([[0], np.cumsum(self.numels)[:-1]]).astype(np.int64).tolist()
+        self.n = int(sum(self.numels))
+        self.device = torch.device(device)
+        self.readout_name = readout_name
+        self.bias = bias
+        self.requires_grad = [True] * len(self.names)
+        self.params = []
+        self._grad_ptrs = []
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.theta = torch.empty(self.n, **f32) if init is None else init
+        self.grad = torch.zeros(self.n, **f32)
+        self.mom = torch.zeros(self.n, **f32) if need_mom else None
+        self.prior = torch.zeros(self.n, **f32) if need_prior else None
+        self.noise = torch.empty(self.n, **f32) if need_noise else None
+        self.attrs = segment_attrs(self.names, readout_name, bias, self.requires_grad)
+        self.runs = build_runs(self.offsets, self.numels, self.attrs, self.n).to(self.device)
+        self.nruns = int(self.runs.shape[0])
+        return self
+
+    # ---------------------------------------------------------------- grads
+    def _bind_grads(self):
+        self._grad_ptrs = []
+        for p, o, k, rg in zip(self.params, self.offsets, self.numels,
+                               [p.requires_grad for p in self.params]):
+            if rg:
+                p.grad = self.grad[o:o + k].view(p.shape)
+                self._grad_ptrs.append(p.grad.data_ptr())
+            else:
+                self._grad_ptrs.append(None)
+
+    def zero_grad(self):
+        """Replaces net.zero_grad(): keep .grad bound to the flat buffer."""
+        self.grad.zero_()
+        for p, ptr in zip(self.params, self._grad_ptrs):
+            if ptr is not None and (p.grad is None or p.grad.data_ptr() != ptr):
+                self._bind_grads()
+                break
+
+    def sync_grads(self):
+        """After backward: if user code replaced a .grad, copy it into the flat buffer."""
+        rebind = False
+        for p, o, k, ptr in zip(self.params, self.offsets, self.numels, self._grad_ptrs):
+            if ptr is None:
+                continue
+            g = p.grad
+            if g is None:
+                self.grad[o:o + k].zero_()
+                rebind = True
+            elif g.data_ptr() != ptr:
+                self.grad[o:o + k].copy_(g.reshape(-1))
+                rebind = True
+        if rebind:
+            self._bind_grads()
+
+    def check_bound(self):
+        """Raise if a parameter no longer aliases the flat theta buffer."""
+        for nm, p, o in zip(self.names, self.params, self.offsets):
+            if p.data.data_ptr() != self.theta.data_ptr() + 4 * o:
+                raise RuntimeError(f"bayesdll_amd: parameter {nm!r} was re-allocated outside the "
+                                   "sampler; rebuild the sampler state")
+
+    # --------------------------------------------------------------- views
+    def views(self, vec):
+        return [vec[o:o + k].view(s) for o, k, s in zip(self.offsets, self.numels, self.shapes)]
+
+    def fill_noise_torch(self, generator=None):
+        """Per-tensor standard-normal draws in named_parameters order: the same
+        generator calls as the reference's torch.randn_like(p) per tensor
+        (methods/csghmc.py:766) — used by the "torch" parity noise mode."""
+        for v, rg in zip(self.views(self.noise), self.requires_grad):
+            if rg:
+                v.normal_(generator=generator)
+        return self.noise
+
+    def segment_table(self):
+        return [(nm, o, k, a) for nm, o, k, a in zip(self.names, self.offsets, self.numels,
+                                                       self.attrs)]
+
+
+def runs_ptr(state):
+    return C.c_void_p(state.runs.data_ptr())
+
+
+def bind_parameters(net):
+    """Rebind `net`'s parameters as views of ONE new flat fp32 buffer (values
+    copied) and drop their grads; returns the buffer.  Used for the evaluation
+    copies whose theta the posterior-sample kernel writes in one sweep."""
+    params = list(net.parameters())
+    n = sum(p.numel() for p in params)
+    dev = params[0].device
+    flat = torch.empty(n, dtype=torch.float32, device=dev)
+    off = 0
+    with torch.no_grad():
+        for p in params:
+            k = p.numel()
+            flat[off:off + k].copy_(p.data.reshape(-1))
+            p.data = flat[off:off + k].view(p.shape)
+            p.grad = None
+            off += k
+    return flat
+
+
+def fill_normal_per_tensor(vec, numels, generator=None):
+    """Per-tensor normal_() over consecutive slices of `vec` (the reference's
+    per-parameter torch.randn_like(p) stream)."""
+    off = 0
+    for k in numels:
+        vec[off:off + k].normal_(generator=generator)
+        off += k
+    return vec

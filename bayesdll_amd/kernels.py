@@ -1,0 +1,104 @@
+"""Python-side calls into the fused HIP kernels (libbdl_sgmcmc.so).
+
+Every scalar is handed over as the float64 value the reference computes on
+the host; ctypes rounds it to fp32 (round-to-nearest), which is exactly the
+cast torch applies to a Python/NumPy scalar at an fp32 op.  Launches go on
+torch's current HIP stream, so ordering with autograd is implicit and no host
+synchronisation happens here.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import _lib as L
+
+# Scalar-division rounding: "true" = x / s (torch CPU, the golden fixtures);
+# "recip" = x * fl(1/s) (torch's HIP kernels divide by a scalar this way).
+DIV_MODE = os.environ.get("BDL_DIV_MODE", "true")
+
+
+def _div_flag(div_mode=None):
+    return L.FLAG_RECIP_DIV if (div_mode or DIV_MODE) == "recip" else 0
+
+
+def sgmcmc_step(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1.0,
+                prior_sig=0.0, sigma2=1.0, n_data=1.0, mu=0.0, first_step=False,
+                momentum=False, collect=L.COLLECT_NONE, mom1=None, mom2=None, collect_a=1.0,
+                collect_b=1.0, seed=0, chain=0, step=0, div_mode=None, noise=None, grad_ready=False):
+    """One fused update over `state` (a FlatState). Asynchronous."""
+    a = L.StepArgs()
+    a.theta = state.theta.data_ptr()
+    a.grad = state.grad.data_ptr()
+    a.mom = None if state.mom is None else state.mom.data_ptr()
+    a.prior_mean = None if state.prior is None else state.prior.data_ptr()
+    nz = noise if noise is not None else state.noise
+    a.noise = None if nz is None else nz.data_ptr()
+    a.mom1 = None if mom1 is None else mom1.data_ptr()
+    a.mom2 = None if mom2 is None else mom2.data_ptr()
+    a.runs = state.runs.data_ptr()
+    a.nruns = state.nruns
+    a.method = int(method)
+    a.noise_mode = int(noise_mode)
+    a.collect = int(collect)
+    a.flags = ((L.FLAG_FIRST_STEP if first_step else 0) | (L.FLAG_MOMENTUM if momentum else 0)
+               | (L.FLAG_GRAD_READY if grad_ready else 0) | _div_flag(div_mode))
+    a.n = state.n
+    a.lr[0], a.lr[1] = float(lrs[0]), float(lrs[1])
+    a.noise_scale[0], a.noise_scale[1] = float(noise_scale[0]), float(noise_scale[1])
+    a.one_minus_alpha = float(one_minus_alpha)
+    a.prior_sig = float(prior_sig)
+    a.sigma2 = float(sigma2)
+    a.n_data = float(n_data)
+    a.mu = float(mu)
+    a.collect_a = float(collect_a)
+    a.collect_b = float(collect_b)
+    a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    a.chain = int(chain) & 0xFFFFFFFFFFFFFFFF
+    a.step = int(step) & 0xFFFFFFFFFFFFFFFF
+    L.check(L.lib().bdl_sgmcmc_step(a, L.current_stream_handle(state.device)), "bdl_sgmcmc_step")
+
+
+def moments_update(theta, mom1, mom2, collect, collect_a=1.0, collect_b=1.0, div_mode=None):
+    """Stand-alone posterior-moment update of flat vectors (no parameter update)."""
+    L.require_hip(theta, "theta")
+    a = L.MomentsArgs()
+    a.theta, a.mom1 = theta.data_ptr(), mom1.data_ptr()
+    a.mom2 = None if mom2 is None else mom2.data_ptr()
+    a.n = theta.numel()
+    a.collect = int(collect)
+    a.flags = _div_flag(div_mode)
+    a.collect_a, a.collect_b = float(collect_a), float(collect_b)
+    L.check(L.lib().bdl_moments_update(a, L.current_stream_handle(theta.device)),
+            "bdl_moments_update")
+
+
+def posterior_sample(out, mom1, mom2, *, var_mode, ratio=1.0, var_floor=1e-12, noise=None,
+                     seed=0, chain=0, step=0):
+    """out = mom1 + sqrt(clamp(var(mom1, mom2), var_floor)) * eps (eps: buffer or Philox)."""
+    L.require_hip(out, "out")
+    a = L.SampleArgs()
+    a.out, a.mom1 = out.data_ptr(), mom1.data_ptr()
+    a.mom2 = None if mom2 is None else mom2.data_ptr()
+    a.noise = None if noise is None else noise.data_ptr()
+    a.n = out.numel()
+    a.var_mode = int(var_mode)
+    a.noise_mode = L.NOISE_BUFFER if noise is not None else L.NOISE_PHILOX
+    a.ratio = float(ratio)
+    a.var_floor = float(var_floor)
+    a.seed, a.chain, a.step = int(seed), int(chain), int(step) & 0xFFFFFFFFFFFFFFFF
+    L.check(L.lib().bdl_posterior_sample(a, L.current_stream_handle(out.device)),
+            "bdl_posterior_sample")
+
+
+def philox_normal(n, seed, chain, step, device="cuda"):
+    """The N(0,1) values the step kernel draws in Philox mode, as a tensor."""
+    out = torch.empty(n, dtype=torch.float32, device=device)
+    L.check(L.lib().bdl_philox_normal(out.data_ptr(), int(n), int(seed), int(chain), int(step),
+                                      L.current_stream_handle(out.device)), "bdl_philox_normal")
+    return out
+
+
+def set_launch_config(blocks_per_cu=0, unroll=0):
+    return L.lib().bdl_set_launch_config(int(blocks_per_cu), int(unroll))

@@ -1,0 +1,245 @@
+"""Benchmark: fused cSGHMC leapfrog update on a ViT-L/32-sized chain (config 4/5).
+
+One step = one cyclical-SGHMC update of a full ViT-L/32 parameter vector
+(306,535,400 fp32, 296 tensors, `heads.head` readout), driven exactly like the
+reference Runner's batch loop (methods/csghmc.py:265-348): alpha(t) from the
+cyclical schedule (M=4 cycles over the run, beta=0.5), noise only on sample
+steps, thinning on the batch index, and the per-cycle Welford accumulation of
+the posterior moments on thinned sample steps — all in the fused HIP kernel.
+Gradients are a synthetic resident buffer (g ~ N(0, 1e-3^2)), re-read every
+step; theta ~ N(0, 0.02^2), v = 0 at step 0.
+
+Multi-GPU (`torch.distributed.run --nproc-per-node N`): one independent chain
+per GPU (seed 42 + rank, Philox chain id = rank); no collective inside the
+timed region; value = total chain-steps / max-over-ranks wall time.
+
+Prints one JSON line (rank 0).  Extra fields: hbm_gbs (algorithmic), the
+per-kernel-kind table with HIP-event timings, roofline of the dominant
+kernel, and the CPU baseline (the oracle's op-for-op torch-CPU restatement of
+the reference update, timed on this host on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BYTES_PER_ELEM = {"explore": 20, "sample": 20, "collect_init": 28, "collect": 36}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--backbone", default="vit_l_32")
+    ap.add_argument("--num-classes", type=int, default=1000)
+    ap.add_argument("--thin", type=int, default=10)
+    ap.add_argument("--cycles", type=int, default=4)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--blocks-per-cu", type=int, default=0)
+    ap.add_argument("--unroll", type=int, default=0)
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist, rank, world, local
+    torch.cuda.set_device(local)
+    return None, 0, 1, local
+
+
+def cpu_baseline(segs, readout, seconds):
+    """The reference csghmc per-tensor update (oracle restatement, torch CPU,
+    torch.randn_like per tensor) on the full ViT-L/32 shapes, timed for a
+    bounded number of steps."""
+    from oracle import sgmcmc_oracle as O
+    threads = len(os.sched_getaffinity(0))
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    params = [torch.randn(s, generator=g) * 0.02 for _, s in segs]
+    grads = [torch.randn(s, generator=g) * 1e-3 for _, s in segs]
+    moms = [torch.zeros(s) for _, s in segs]
+    names = [nm for nm, _ in segs]
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        moms = O.csghmc_step_cpu(params, grads, moms, names, readout, [1e-4, 1e-2], 1.0, 0.18,
+                                 1840.0, 0.01, True)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or steps >= 50:
+            break
+    cpu_model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": steps / el, "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} full ViT-L/32 cSGHMC updates (296 tensors, 306,535,400 params, "
+                      f"randn_like noise) in {el:.1f} s on {cpu_model}"}
+
+
+def main():
+    a = parse()
+    dist, rank, world, local = dist_setup()
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.cyclical import CyclicalSGMCMC
+    from bayesdll_amd.flat import FlatState
+    from bayesdll_amd.shapes import segments
+
+    if a.blocks_per_cu or a.unroll:
+        K.set_launch_config(a.blocks_per_cu, a.unroll)
+    segs, readout = segments(a.backbone, a.num_classes)
+    dev = torch.device("cuda", local)
+    st = FlatState.from_segments(segs, readout, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(42 + rank)
+    st.theta.normal_(0.0, 0.02, generator=gen)
+    st.grad.normal_(0.0, 1e-3, generator=gen)
+    n = st.n
+
+    # config 4 hyper-parameters
+    lr, lr_head, alpha, nd, ND, Ninflate, prior_sig = 1e-4, 1e-2, 0.18, 0.01, 1840, 1.0, 1.0
+    N = ND * Ninflate
+    total = a.warmup + a.steps
+    sched = CyclicalSGMCMC(lr, a.cycles, 1, 0.5)  # one "epoch" of `total` batches
+    m1s, m2s, spc = {}, {}, {}
+
+    def plan(k):
+        cur = sched.calculate_lr(0, k, total)
+        ss = sched.should_sample(0, k, total) and k % a.thin == 0
+        kind, collect, spec = ("sample" if ss else "explore"), L.COLLECT_NONE, None
+        if ss:
+            c = sched.get_cycle_number(0, k, total)
+            if c not in m1s:
+                m1s[c] = torch.empty(n, dtype=torch.float32, device=dev)
+                m2s[c] = torch.empty(n, dtype=torch.float32, device=dev)
+                spec = (L.COLLECT_WELFORD_INIT, c, 1.0, 1)
+                kind = "collect_init"
+            else:
+                cnt = spc[c] + 1
+                spec = (L.COLLECT_WELFORD, c, float(cnt), cnt)
+                kind = "collect"
+        return cur, ss, kind, spec
+
+    def step(k, ev=None):
+        cur, ss, kind, spec = plan(k)
+        lrs = (cur, cur * (lr_head / lr))
+        ns = [nd * np.sqrt(2 * alpha * x) / N for x in lrs]
+        ckind, m1, m2, ca = L.COLLECT_NONE, None, None, 1.0
+        if spec is not None:
+            ckind, c, ca, cnt = spec
+            m1, m2 = m1s[c], m2s[c]
+        if ev is not None:
+            ev[0].record()
+        K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=ns,
+                      noise_mode=L.NOISE_PHILOX if ss else L.NOISE_NONE,
+                      one_minus_alpha=1 - alpha, prior_sig=prior_sig, collect=ckind, mom1=m1,
+                      mom2=m2, collect_a=ca, seed=42 + rank, chain=rank, step=k)
+        if ev is not None:
+            ev[1].record()
+        if spec is not None:  # the reference's double increment (quirk Q2)
+            spc[c] = cnt + 1
+        return kind
+
+    for k in range(a.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(a.steps)]
+    kinds = []
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        kinds.append(step(a.warmup + i, events[i]))
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(st.theta[:1 << 20]).all()
+
+    per = {}
+    for kind, (e0, e1) in zip(kinds, events):
+        per.setdefault(kind, []).append(e0.elapsed_time(e1))
+    table = {}
+    for kind, ms in per.items():
+        avg = float(np.mean(ms))
+        gbs = BYTES_PER_ELEM[kind] * n / (avg * 1e-3) / 1e9
+        table[kind] = {"launches": len(ms), "avg_ms": round(avg, 4),
+                       "p10_ms": round(float(np.percentile(ms, 10)), 4),
+                       "p90_ms": round(float(np.percentile(ms, 90)), 4),
+                       "bytes_per_elem": BYTES_PER_ELEM[kind], "gbs": round(gbs, 1)}
+    dominant = max(table, key=lambda k: table[k]["launches"] * table[k]["avg_ms"])
+    dom = table[dominant]
+    alg_bytes = dom["bytes_per_elem"] * n
+    achieved = alg_bytes / (dom["avg_ms"] * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(a.traffic):
+        try:
+            tj = json.load(open(a.traffic))
+            traffic = tj.get(a.backbone, {}).get(dominant)
+        except Exception:
+            traffic = None
+    total_bytes = sum(BYTES_PER_ELEM[k] * n for k in kinds)
+    hbm_gbs = total_bytes / elapsed / 1e9  # per rank, algorithmic, wall-clock
+
+    out = {
+        "metric": "SG-HMC leapfrog steps/sec & HBM GB/s on ViT-L/32 params, 1/2/4/8 MI355X",
+        "value": round(world * a.steps / elapsed, 2),
+        "unit": "steps/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (random-init theta, resident synthetic grad buffer)",
+        "config": {"workload": f"{a.backbone} cSGHMC fused leapfrog update (config 4/5)",
+                   "params": n, "tensors": len(segs), "readout": readout,
+                   "cycles": a.cycles, "thin": a.thin, "beta": 0.5, "noise": "philox",
+                   "parallelism": f"{world} independent chains (1/GPU)"},
+        "hbm_gbs": round(hbm_gbs * world, 1),
+        "kernels": table,
+        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
+                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+                     "traffic": traffic,
+                     "alg_bytes_per_launch": alg_bytes},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(segs, readout, a.cpu_baseline_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -100,6 +100,8 @@ typedef enum bdl_collect {
 #define BDL_FLAG_FIRST_STEP 0x1  /* SGD momentum buffer does not exist yet: buf = grad */
 #define BDL_FLAG_RECIP_DIV 0x2   /* divide by a scalar as x*(1/s) (torch-on-GPU), else x/s (torch CPU) */
 #define BDL_FLAG_MOMENTUM 0x4    /* SGD momentum != 0: maintain args.mom as SGD buffer */
+#define BDL_FLAG_GRAD_READY 0x8  /* BDL_SGLD/BDL_SGHMC: grad already holds the sampler gradient
+                                    (e.g. clipped after a *_GRAD call): apply the SGD step only */
 
 /* One parameter tensor in named_parameters order (host input to bdl_build_runs). */
 typedef struct bdl_segment {

@@ -1,0 +1,133 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol the
+header declares, the ctypes mirrors match the C struct layouts (compiled with
+gcc from include/bdl_sgmcmc.h), and the host-only run builder behaves."""
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "bdl_sgmcmc.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(bdl_\w+)\(", txt, re.M)))
+
+
+def test_header_declares_expected_api():
+    assert declared_functions() == sorted([
+        "bdl_version", "bdl_last_error", "bdl_build_runs", "bdl_sgmcmc_step",
+        "bdl_moments_update", "bdl_posterior_sample", "bdl_philox_normal",
+        "bdl_set_launch_config"])
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    from bayesdll_amd import _lib as L
+    h = L.lib()
+    for name in declared_functions():
+        assert hasattr(h, name), name
+    assert set(declared_functions()) == set(L.EXPORTS)
+    assert h.bdl_version() == L.ABI_VERSION
+
+
+def _c_layout():
+    src = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "bdl_sgmcmc.h"
+#define P(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
+int main(void) {
+  printf("bdl_segment %zu\nbdl_run %zu\nbdl_step_args %zu\nbdl_moments_args %zu\nbdl_sample_args %zu\n",
+         sizeof(bdl_segment), sizeof(bdl_run), sizeof(bdl_step_args), sizeof(bdl_moments_args),
+         sizeof(bdl_sample_args));
+  P(bdl_step_args, runs) P(bdl_step_args, nruns) P(bdl_step_args, n) P(bdl_step_args, lr)
+  P(bdl_step_args, noise_scale) P(bdl_step_args, mu) P(bdl_step_args, collect_b)
+  P(bdl_step_args, seed) P(bdl_step_args, step) P(bdl_moments_args, collect_a)
+  P(bdl_sample_args, ratio) P(bdl_sample_args, step) P(bdl_run, attr) P(bdl_segment, attr)
+  return 0;
+}
+"""
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "probe.c")
+        exe = os.path.join(d, "probe")
+        open(c, "w").write(src)
+        subprocess.check_call(["gcc", "-std=c99", "-I", os.path.dirname(HEADER), c, "-o", exe])
+        out = subprocess.check_output([exe]).decode()
+    return dict(line.rsplit(" ", 1) for line in out.strip().splitlines())
+
+
+def test_ctypes_layout_matches_c_header():
+    from bayesdll_amd import _lib as L
+    lay = {k: int(v) for k, v in _c_layout().items()}
+    assert lay["bdl_segment"] == C.sizeof(L.Segment)
+    assert lay["bdl_run"] == C.sizeof(L.Run)
+    assert lay["bdl_step_args"] == C.sizeof(L.StepArgs)
+    assert lay["bdl_moments_args"] == C.sizeof(L.MomentsArgs)
+    assert lay["bdl_sample_args"] == C.sizeof(L.SampleArgs)
+    for key, v in lay.items():
+        if "." not in key:
+            continue
+        struct, field = key.split(".")
+        cls = {"bdl_step_args": L.StepArgs, "bdl_moments_args": L.MomentsArgs,
+               "bdl_sample_args": L.SampleArgs, "bdl_run": L.Run, "bdl_segment": L.Segment}[struct]
+        assert getattr(cls, field).offset == v, key
+
+
+def test_build_runs_merges_equal_attributes():
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd.flat import build_runs, segment_attrs
+    names = ["a.weight", "a.bias", "b.weight", "b.bias", "classifier.weight", "classifier.bias"]
+    numels = [10, 3, 7, 1, 5, 2]
+    offsets = [0, 10, 13, 20, 21, 26]
+    # informative: only the head boundary matters
+    attrs = segment_attrs(names, "classifier", "informative", [True] * 6)
+    runs = build_runs(offsets, numels, attrs, 28)
+    assert runs.tolist() == [[21, L.ATTR_PRIOR], [28, L.ATTR_PRIOR | L.ATTR_HEAD]]
+    # uninformative bias: bias segments lose the prior bit
+    attrs = segment_attrs(names, "classifier", "uninformative", [True] * 6)
+    runs = build_runs(offsets, numels, attrs, 28)
+    assert runs.tolist() == [[10, 2], [13, 0], [20, 2], [21, 0], [26, 3], [28, 1]]
+    # frozen parameter -> skip run; trailing gap -> skip
+    attrs = segment_attrs(names, "classifier", "informative", [True, False] + [True] * 4)
+    runs = build_runs(offsets, numels, attrs, 30)
+    assert runs.tolist() == [[10, 2], [13, 6], [21, 2], [28, 3], [30, 4]]
+
+
+def test_build_runs_rejects_bad_tables():
+    from bayesdll_amd.flat import build_runs
+    with pytest.raises(RuntimeError, match="overlap"):
+        build_runs([0, 5], [10, 3], [0, 0], 20)
+    with pytest.raises(RuntimeError, match="exceed"):
+        build_runs([0], [30], [0], 20)
+
+
+def test_empty_vector_is_one_skip_run():
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd.flat import build_runs
+    assert build_runs([], [], [], 0).tolist() == [[0, L.ATTR_SKIP]]
+
+
+def test_product_refuses_cpu_tensors():
+    """No CPU fallback: a net on the CPU is rejected before any kernel call."""
+    from fakenet import FakeNet
+    from bayesdll_amd.flat import FlatState
+    with pytest.raises(RuntimeError, match="HIP device"):
+        FlatState(FakeNet())
+
+
+def test_step_rejects_null_and_misaligned_pointers_without_launching():
+    from bayesdll_amd import _lib as L
+    a = L.StepArgs()
+    a.n = 16
+    a.method = L.CSGHMC
+    rc = L.lib().bdl_sgmcmc_step(a, None)
+    assert rc == -1 and b"required" in L.lib().bdl_last_error()
+    a.theta, a.grad, a.mom, a.runs, a.nruns = 0x1004, 0x2000, 0x3000, 0x4000, 1
+    rc = L.lib().bdl_sgmcmc_step(a, None)
+    assert rc == -2 and b"aligned" in L.lib().bdl_last_error()
+    a.theta, a.method = 0x1000, 9
+    assert L.lib().bdl_sgmcmc_step(a, None) == -3

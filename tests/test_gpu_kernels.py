@@ -1,0 +1,282 @@
+"""Kernel-level GPU tests of libbdl_sgmcmc.so through the C-ABI.
+
+* full-size parity (ViT-L/32: 306,535,400 params, 296 tensors): one fused step
+  vs the reference's per-tensor op sequence executed with torch ops on the same
+  GPU, same noise — bit-exact (the kernel rounds every op where torch does);
+* edge sizes (n = 1, 3, 4, 5, 17, 4097, ...) and run boundaries inside float4
+  groups, for every method;
+* Philox noise: determinism, key separation, moments, KS vs N(0,1), and that
+  the step in Philox mode equals the step fed the same draws as a buffer;
+* posterior-sample and moment kernels vs their torch formulas.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+
+
+def _state(segments, readout, bias="informative", seed=0, **kw):
+    from bayesdll_amd.flat import FlatState
+    st = FlatState.from_segments(segments, readout, bias=bias, device=DEV, **kw)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(seed)
+    st.theta.normal_(0.0, 0.02, generator=g)
+    st.grad.normal_(0.0, 1e-3, generator=g)
+    if st.mom is not None:
+        st.mom.normal_(0.0, 1e-4, generator=g)
+    if st.prior is not None:
+        st.prior.normal_(0.0, 0.02, generator=g)
+    if st.noise is not None:
+        st.noise.normal_(generator=g)
+    return st
+
+
+# ------------------------------------------------------------ torch references
+def ref_csghmc(st, lrs, ns, alpha, prior_sig, add_noise):
+    """methods/csghmc.py:759-778 with torch ops, per tensor, on the device."""
+    th, v = st.theta.clone(), st.mom.clone()
+    for (o, k, a) in zip(st.offsets, st.numels, st.attrs):
+        h = 1 if a & 1 else 0
+        p, g, vv = th[o:o + k], st.grad[o:o + k], v[o:o + k]
+        gu = g + prior_sig * p
+        nz = ns[h] * st.noise[o:o + k]
+        vn = vv * (1 - alpha) - lrs[h] * gu
+        if add_noise:
+            vn = vn + nz
+        vv.copy_(vn)
+        p.add_(vn)
+    return th, v
+
+
+def ref_sgld(st, lrs, ns, sigma, N, mu, first, recip):
+    """methods/sgld.py:476-484 + SGD(momentum) with torch ops on the device."""
+    th, buf = st.theta.clone(), st.mom.clone()
+    for (o, k, a) in zip(st.offsets, st.numels, st.attrs):
+        h = 1 if a & 1 else 0
+        p, p0, g = th[o:o + k], st.prior[o:o + k], st.grad[o:o + k]
+        nz = ns[h] * st.noise[o:o + k]
+        if a & 2:
+            d = p - p0
+            if recip:  # torch's HIP kernel: x * fl(1/s)
+                gp = g + (d / (sigma ** 2) / N + nz)
+            else:
+                s2 = torch.tensor(np.float32(sigma ** 2))
+                nn_ = torch.tensor(np.float32(N))
+                gp = g + ((d.cpu() / s2 / nn_).to(DEV) + nz)
+        else:
+            gp = g + nz
+        b = buf[o:o + k]
+        if mu != 0:
+            if first:
+                b.copy_(gp)
+            else:
+                b.mul_(mu).add_(gp)
+            gp = b
+        p.add_(gp, alpha=-lrs[h])
+    return th, buf
+
+
+# ------------------------------------------------------------------- tests
+def test_full_size_vit_csghmc_step_bitexact_vs_torch():
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.shapes import vit_l_32
+    segs, readout = vit_l_32()
+    st = _state(segs, readout, need_noise=True)
+    assert st.n == 306_535_400 and len(segs) == 296
+    lrs, alpha, psig = (1e-4, 1e-2), 0.18, 1.0
+    N, nd = 1840.0, 0.01
+    ns = [nd * np.sqrt(2 * alpha * lr) / N for lr in lrs]
+    for add_noise in (False, True):
+        th_ref, v_ref = ref_csghmc(st, lrs, ns, alpha, psig, add_noise)
+        K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=ns,
+                      noise_mode=L.NOISE_BUFFER if add_noise else L.NOISE_NONE,
+                      one_minus_alpha=1 - alpha, prior_sig=psig)
+        torch.cuda.synchronize()
+        assert torch.equal(st.theta, th_ref)
+        assert torch.equal(st.mom, v_ref)
+
+
+def test_full_size_vit_sgld_uninformative_many_runs():
+    """296 tensors with uninformative biases -> ~300 runs; the recip-division
+    path is bit-exact with torch's own device kernels."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.shapes import vit_l_32
+    segs, readout = vit_l_32()
+    st = _state(segs, readout, bias="uninformative", need_prior=True, need_noise=True, seed=1)
+    assert st.nruns > 290
+    lrs, sigma, N, nd, mu = (1e-4, 1e-2), 1.0, 1840.0 * 1e3, 0.01, 0.5
+    ns = [nd * np.sqrt(2 / (N * lr)) for lr in lrs]
+    for first in (True, False):
+        th_ref, b_ref = ref_sgld(st, lrs, ns, sigma, N, mu, first, recip=True)
+        K.sgmcmc_step(st, L.SGLD, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_BUFFER,
+                      prior_sig=sigma, sigma2=sigma ** 2, n_data=N, mu=mu, first_step=first,
+                      momentum=True, div_mode="recip")
+        torch.cuda.synchronize()
+        # add_(alpha=-lr) may or may not be contracted to an FMA by torch's
+        # device kernel: allow 1 ulp on theta, exact on the buffer
+        assert torch.equal(st.mom, b_ref)
+        np.testing.assert_allclose(st.theta.cpu().numpy(), th_ref.cpu().numpy(), rtol=2e-7,
+                                   atol=1e-12)
+        st.theta.copy_(th_ref)
+
+
+SMALL = [1, 3, 4, 5, 7, 17, 64, 1023, 4097, 65537]
+
+
+@pytest.mark.parametrize("n", SMALL)
+def test_edge_sizes_csghmc_and_sgld(n):
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    # split n into odd-sized tensors with a trailing head + bias
+    rng = np.random.default_rng(n)
+    cuts = sorted(set(rng.integers(1, n, size=min(5, max(n - 1, 0))).tolist())) if n > 1 else []
+    bounds = [0] + cuts + [n]
+    segs = []
+    for i in range(len(bounds) - 1):
+        k = bounds[i + 1] - bounds[i]
+        name = ("fc." if i == len(bounds) - 2 else f"l{i}.") + ("bias" if i % 2 else "weight")
+        segs.append((name, (k,)))
+    st = _state(segs, "fc", need_noise=True, need_prior=True)
+    lrs, alpha = (0.01, 0.05), 0.1
+    ns = [0.3, 0.7]
+    th_ref, v_ref = ref_csghmc(st, lrs, ns, alpha, 0.5, True)
+    K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_BUFFER,
+                  one_minus_alpha=1 - alpha, prior_sig=0.5)
+    torch.cuda.synchronize()
+    assert torch.equal(st.theta, th_ref) and torch.equal(st.mom, v_ref)
+
+    st2 = _state(segs, "fc", bias="uninformative", need_noise=True, need_prior=True, seed=5)
+    th_ref, b_ref = ref_sgld(st2, lrs, ns, 0.8, 50.0, 0.9, False, recip=False)
+    K.sgmcmc_step(st2, L.SGLD, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_BUFFER, sigma2=0.8 ** 2,
+                  n_data=50.0, mu=0.9, momentum=True, first_step=False)
+    torch.cuda.synchronize()
+    assert torch.equal(st2.mom, b_ref)
+    np.testing.assert_allclose(st2.theta.cpu().numpy(), th_ref.cpu().numpy(), rtol=2e-7, atol=0)
+
+
+def test_zero_length_is_a_noop():
+    from bayesdll_amd import _lib as L
+    a = L.StepArgs()
+    a.n = 0
+    assert L.lib().bdl_sgmcmc_step(a, None) == 0
+
+
+def test_philox_determinism_and_key_separation():
+    from bayesdll_amd.kernels import philox_normal
+    n = 1 << 20
+    a = philox_normal(n, 42, 0, 7)
+    b = philox_normal(n, 42, 0, 7)
+    assert torch.equal(a, b)
+    for other in (philox_normal(n, 43, 0, 7), philox_normal(n, 42, 1, 7),
+                  philox_normal(n, 42, 0, 8)):
+        c = torch.corrcoef(torch.stack([a, other]))[0, 1].item()
+        assert abs(c) < 6 / math.sqrt(n)
+        assert not torch.equal(a, other)
+    # prefix consistency: element i does not depend on n
+    assert torch.equal(philox_normal(1001, 42, 0, 7), a[:1001])
+
+
+def test_philox_moments_and_ks():
+    from scipy import stats
+    from bayesdll_amd.kernels import philox_normal
+    n = 1 << 22
+    z = philox_normal(n, 1234, 3, 99).double()
+    assert abs(z.mean().item()) < 5 / math.sqrt(n)
+    assert abs(z.var().item() - 1) < 5 * math.sqrt(2 / n)
+    assert abs(((z ** 3).mean()).item()) < 5 * math.sqrt(15 / n)
+    assert abs(((z ** 4).mean()).item() - 3) < 5 * math.sqrt(96 / n)
+    assert torch.isfinite(z).all()
+    ks = stats.kstest(z[:1 << 20].cpu().numpy(), "norm")
+    assert ks.pvalue > 1e-4, ks
+
+
+def test_philox_step_equals_buffer_step():
+    """The step in Philox mode consumes exactly bdl_philox_normal's stream."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.shapes import mlp_mnist
+    segs, readout = mlp_mnist()
+    a = _state(segs, readout, need_noise=True, seed=3)
+    b = _state(segs, readout, need_noise=True, seed=3)
+    kw = dict(lrs=(1e-3, 1e-2), noise_scale=(1e-2, 3e-2), one_minus_alpha=0.82, prior_sig=1.0,
+              seed=42, chain=5, step=123)
+    K.sgmcmc_step(a, L.CSGHMC, noise_mode=L.NOISE_PHILOX, **kw)
+    b.noise.copy_(K.philox_normal(b.n, 42, 5, 123))
+    K.sgmcmc_step(b, L.CSGHMC, noise_mode=L.NOISE_BUFFER, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(a.theta, b.theta) and torch.equal(a.mom, b.mom)
+
+
+def test_fused_welford_and_running_mean_match_torch():
+    """Collect variants: the moments use the UPDATED theta, as the reference
+    (parameters_to_vector after the step)."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.shapes import mlp_mnist
+    segs, readout = mlp_mnist()
+    st = _state(segs, readout, need_noise=True, seed=9)
+    m1 = torch.randn(st.n, device=DEV)
+    m2 = torch.rand(st.n, device=DEV)
+    kw = dict(lrs=(1e-3, 1e-2), noise_scale=(1e-2, 3e-2), one_minus_alpha=0.82, prior_sig=1.0)
+    th_ref, _ = ref_csghmc(st, kw["lrs"], kw["noise_scale"], 0.18, 1.0, True)
+    e1, e2 = m1.clone(), m2.clone()
+    d = th_ref - e1
+    e1 += d / 5
+    d2 = th_ref - e1
+    e2 += d * d2
+    K.sgmcmc_step(st, L.CSGHMC, noise_mode=L.NOISE_BUFFER, collect=L.COLLECT_WELFORD, mom1=m1,
+                  mom2=m2, collect_a=5.0, div_mode="recip", **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(st.theta, th_ref)
+    assert torch.equal(m1, e1) and torch.equal(m2, e2)
+
+    x = torch.randn(st.n, device=DEV)
+    a1, a2 = torch.randn(st.n, device=DEV), torch.rand(st.n, device=DEV)
+    r1 = (x + 3 * a1) / 4
+    r2 = (x ** 2 + 3 * a2) / 4
+    K.moments_update(x, a1, a2, L.COLLECT_MEAN, 3.0, 4.0, div_mode="recip")
+    torch.cuda.synchronize()
+    assert torch.equal(a1, r1) and torch.equal(a2, r2)
+    b1, b2 = torch.empty_like(x), torch.empty_like(x)
+    K.moments_update(x, b1, b2, L.COLLECT_MEAN_INIT)
+    torch.cuda.synchronize()
+    assert torch.equal(b1, x * 1.0) and torch.equal(b2, x ** 2)
+
+
+def test_posterior_sample_matches_torch_formula():
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    n = 1_000_003
+    m1 = torch.randn(n, device=DEV)
+    m2 = m1 ** 2 + torch.rand(n, device=DEV) * 0.1
+    m2[::7] = m1[::7] ** 2 - 1e-3  # negative variance -> clamp to 1e-12
+    eps = torch.randn(n, device=DEV)
+    ratio = 5 / 4
+    var = (ratio * (m2 - m1 ** 2)).clamp_(min=1e-12)
+    ref = m1 + var.sqrt() * eps
+    out = torch.empty_like(m1)
+    K.posterior_sample(out, m1, m2, var_mode=L.VAR_RAW_MOMENTS, ratio=ratio, noise=eps)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    # Welford form and single-sample form
+    var = (m2 / 3).clamp_(min=1e-12)
+    K.posterior_sample(out, m1, m2, var_mode=L.VAR_WELFORD, ratio=3.0, noise=eps)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(out.cpu().numpy(), (m1 + var.sqrt() * eps).cpu().numpy(),
+                               rtol=1e-6, atol=1e-7)
+    K.posterior_sample(out, m1, None, var_mode=L.VAR_GIVEN, noise=eps)
+    torch.cuda.synchronize()
+    assert torch.equal(out, m1 + torch.full_like(m1, 1e-12).sqrt() * eps)
