@@ -76,7 +76,7 @@ EXPORTS = {
     "bdl_posterior_sample": (C.c_int, [C.POINTER(SampleArgs), C.c_void_p]),
     "bdl_philox_normal": (C.c_int, [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint64,
                                     C.c_void_p]),
-    "bdl_set_launch_config": (C.c_int, [C.c_int32, C.c_int32]),
+    "bdl_set_launch_config": (C.c_int, [C.c_int32, C.c_int32, C.c_int32]),
 }
 
 _lib = None

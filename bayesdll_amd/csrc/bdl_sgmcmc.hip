@@ -45,8 +45,12 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes
 
 // Tunables (bdl_set_launch_config).  blocks_per_cu * 256 CUs workgroups, each
 // lane keeps kUnroll float4 groups in flight per iteration.
-int g_blocks_per_cu = 4;
+// Defaults from the gfx950 sweep (tools/sweep.py, profiles/r01/sweep_*.log):
+// grid-stride with 2 workgroups/CU and 2 float4 groups in flight per lane,
+// non-temporal 16-B loads and stores, measured best on every kernel kind.
+int g_blocks_per_cu = 2;
 int g_unroll = 2;
+int g_grid_stride = 1;  // 0: one contiguous span per block; 1: grid-stride sweep
 
 int device_cu_count() {
   static int cached[64] = {0};
@@ -111,8 +115,36 @@ __device__ __forceinline__ float4 philox_normal4(uint64_t group, uint64_t seed, 
 // Vector helpers: a float4 "group" covers flat elements [4g, 4g+4).  Only the
 // very last group of a vector can be partial; it takes the guarded path.
 // ---------------------------------------------------------------------------
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// 16-B vector access.  Streaming (non-temporal) policy per direction:
+// -DBDL_NT_LOAD / -DBDL_NT_STORE (or -DBDL_NT for both; the default build).
+// Every vector is touched once per step and is far larger than the 256 MiB
+// Infinity Cache, so nothing is lost by not keeping lines resident.
+#ifdef BDL_NT
+#define BDL_NT_LOAD 1
+#define BDL_NT_STORE 1
+#endif
+__device__ __forceinline__ float4 vload(const float* p) {
+#ifdef BDL_NT_LOAD
+  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+#else
+  const f4v v = *reinterpret_cast<const f4v*>(p);
+#endif
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ void vstore(float* p, float4 x) {
+  const f4v v = {x.x, x.y, x.z, x.w};
+#ifdef BDL_NT_STORE
+  __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
+#else
+  *reinterpret_cast<f4v*>(p) = v;
+#endif
+}
+
 __device__ __forceinline__ float4 ld4(const float* __restrict__ p, int64_t e, int64_t n) {
-  if (e + 4 <= n) return *reinterpret_cast<const float4*>(p + e);
+  if (e + 4 <= n) return vload(p + e);
   float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
   if (e + 0 < n) v.x = p[e + 0];
   if (e + 1 < n) v.y = p[e + 1];
@@ -122,7 +154,7 @@ __device__ __forceinline__ float4 ld4(const float* __restrict__ p, int64_t e, in
 
 __device__ __forceinline__ void st4(float* __restrict__ p, int64_t e, int64_t n, float4 v) {
   if (e + 4 <= n) {
-    *reinterpret_cast<float4*>(p + e) = v;
+    vstore(p + e, v);
     return;
   }
   if (e + 0 < n) p[e + 0] = v.x;
@@ -288,8 +320,21 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
 
   const int64_t n = a.n;
   const int64_t ngroups = (n + 3) >> 2;
-  const int64_t g0 = (int64_t)blockIdx.x * a.groups_per_block;
-  const int64_t g1 = min(g0 + a.groups_per_block, ngroups);
+  // Two sweep orders: each block owns one contiguous span (groups_per_block >
+  // 0), or all blocks advance through the vector together (grid-stride,
+  // groups_per_block == 0).  Either way a lane's groups only move forward, so
+  // its run cursor advances monotonically.
+  constexpr int64_t kIter = (int64_t)kBlock * UNROLL;
+  int64_t g0, g1, gstep;
+  if (a.groups_per_block > 0) {
+    g0 = (int64_t)blockIdx.x * a.groups_per_block;
+    g1 = min(g0 + a.groups_per_block, ngroups);
+    gstep = kIter;
+  } else {
+    g0 = (int64_t)blockIdx.x * kIter;
+    g1 = ngroups;
+    gstep = (int64_t)gridDim.x * kIter;
+  }
   if (g0 >= g1) return;
 
   // Block-uniform run search for the span start; each lane then advances.
@@ -297,7 +342,7 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
   int64_t run_hi = a.runs[r].end;
   uint32_t run_attr = a.runs[r].attr;
 
-  for (int64_t gb = g0; gb < g1; gb += (int64_t)kBlock * UNROLL) {
+  for (int64_t gb = g0; gb < g1; gb += gstep) {
     float4 th[UNROLL], g[UNROLL], v[UNROLL], t0[UNROLL], ep[UNROLL], m1[UNROLL], m2[UNROLL];
     int64_t e[UNROLL];
     bool act[UNROLL];
@@ -557,7 +602,7 @@ StepKernel pick_step(int method, int noise, int collect, int unroll) {
 
 int grid_for(int64_t ngroups, int per_block_groups) {
   const int64_t want = (ngroups + per_block_groups - 1) / per_block_groups;
-  const int64_t cap = (int64_t)device_cu_count() * 8;
+  const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
   return (int)std::max<int64_t>(1, std::min(want, cap));
 }
 
@@ -569,10 +614,11 @@ int bdl_version(void) { return BDL_ABI_VERSION; }
 
 const char* bdl_last_error(void) { return g_last_error.c_str(); }
 
-int bdl_set_launch_config(int32_t blocks_per_cu, int32_t unroll) {
-  const int prev = (g_blocks_per_cu << 16) | g_unroll;
-  g_blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : 4;
+int bdl_set_launch_config(int32_t blocks_per_cu, int32_t unroll, int32_t grid_stride) {
+  const int prev = (g_grid_stride << 24) | (g_blocks_per_cu << 8) | g_unroll;
+  g_blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : 2;
   g_unroll = (unroll == 1 || unroll == 2 || unroll == 4) ? unroll : 2;
+  g_grid_stride = grid_stride > 0 ? 1 : 0;
   return prev;
 }
 
@@ -667,7 +713,7 @@ int bdl_sgmcmc_step(const bdl_step_args* s, void* stream) {
   a.nruns = s->nruns;
   a.flags = s->flags;
   a.n = s->n;
-  a.groups_per_block = iters_per_block * per_iter;
+  a.groups_per_block = g_grid_stride ? 0 : iters_per_block * per_iter;
   a.lr0 = s->lr[0];
   a.lr1 = s->lr[1];
   a.ns0 = s->noise_scale[0];

@@ -100,5 +100,5 @@ def philox_normal(n, seed, chain, step, device="cuda"):
     return out
 
 
-def set_launch_config(blocks_per_cu=0, unroll=0):
-    return L.lib().bdl_set_launch_config(int(blocks_per_cu), int(unroll))
+def set_launch_config(blocks_per_cu=0, unroll=0, grid_stride=0):
+    return L.lib().bdl_set_launch_config(int(blocks_per_cu), int(unroll), int(grid_stride))

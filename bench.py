@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--blocks-per-cu", type=int, default=0)
     ap.add_argument("--unroll", type=int, default=0)
+    ap.add_argument("--grid-stride", type=int, default=-1)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -71,7 +72,8 @@ def cpu_baseline(segs, readout, seconds):
     torch.randn_like per tensor) on the full ViT-L/32 shapes, timed for a
     bounded number of steps."""
     from oracle import sgmcmc_oracle as O
-    threads = len(os.sched_getaffinity(0))
+    # the box's CPU share (OMP_NUM_THREADS is set to it), not the whole machine
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
     params = [torch.randn(s, generator=g) * 0.02 for _, s in segs]
@@ -108,8 +110,8 @@ def main():
     from bayesdll_amd.flat import FlatState
     from bayesdll_amd.shapes import segments
 
-    if a.blocks_per_cu or a.unroll:
-        K.set_launch_config(a.blocks_per_cu, a.unroll)
+    if a.blocks_per_cu or a.unroll or a.grid_stride >= 0:
+        K.set_launch_config(a.blocks_per_cu, a.unroll, max(a.grid_stride, 0))
     segs, readout = segments(a.backbone, a.num_classes)
     dev = torch.device("cuda", local)
     st = FlatState.from_segments(segs, readout, device=dev)

@@ -207,9 +207,12 @@ int bdl_posterior_sample(const bdl_sample_args* args, void* hip_stream);
 int bdl_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t chain,
                       uint64_t step, void* hip_stream);
 
-/* Launch geometry override for tuning (0 = default). Returns the previous
- * value packed as (blocks_per_cu << 16) | unroll. Not thread-safe; test only. */
-int bdl_set_launch_config(int32_t blocks_per_cu, int32_t unroll);
+/* Launch geometry override for tuning (0 = default): workgroups per CU, float4
+ * groups in flight per lane (1, 2, 4; the cSGHMC kernel only), and the sweep
+ * order (0 = one contiguous span per workgroup, 1 = grid-stride).  Returns the
+ * previous value packed as (grid_stride << 24) | (blocks_per_cu << 8) | unroll.
+ * Process-global, not thread-safe; for tuning and tests. */
+int bdl_set_launch_config(int32_t blocks_per_cu, int32_t unroll, int32_t grid_stride);
 
 #ifdef __cplusplus
 }

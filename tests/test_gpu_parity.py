@@ -157,6 +157,8 @@ def test_same_seed_matches_reference_update_on_gpu(method, bias):
     n = numel_of(TOY_SEGMENTS)
     cfg = dict(init=init_vector(3, n, 0.5), prior=init_vector(4, n, 0.3), lr=0.03, lr_head=0.07,
                prior_sig=0.9, alpha=0.2, N=60.0, nd=0.7, bias=bias, momentum=0.5)
+    if method == "sghmc":
+        cfg["momentum"] = 0.0  # sghmc's Runner steps SGD with momentum 0 (methods/sghmc.py:53-57)
     ref = _reference_gpu_chain(method, 6, 77, 4242, cfg)
     got = _product_gpu_chain(method, 6, 77, 4242, cfg, div_mode="recip")
     assert rel_err(got, ref) <= RTOL
