@@ -39,13 +39,9 @@ def default_noise_mode():
 
 
 def default_chain():
-    try:
-        import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized():
-            return dist.get_rank()
-    except Exception:  # pragma: no cover
-        pass
-    return 0
+    """Chain id = process rank when torch.distributed is initialised."""
+    from . import chains
+    return chains.rank()
 
 
 class FusedModelBase(nn.Module):

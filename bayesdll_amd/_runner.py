@@ -23,6 +23,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib as L
+from . import chains
 from . import kernels as K
 from .flat import bind_parameters, fill_normal_per_tensor
 
@@ -58,25 +59,12 @@ class PosteriorDraw:
 
 
 def chain_world():
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized():
-        return dist.get_world_size()
-    return 1
+    return chains.world()
 
 
 def chain_average_logprob(logp):
-    """log of the across-chain mean predictive probability (one RCCL all_reduce).
-
-    Per chain, logp = log p_chain(y|x) ([B, C]); returns log((1/K) sum_k p_k),
-    the multi-chain analogue of logsumexp(...) - log(nst) (methods/sgld.py:300).
-    """
-    import torch.distributed as dist
-    k = chain_world()
-    if k == 1:
-        return logp
-    p = logp.exp()
-    dist.all_reduce(p, op=dist.ReduceOp.SUM)
-    return (p / k).log()
+    """Across-chain posterior-predictive average (bayesdll_amd.chains)."""
+    return chains.average_predictive(logp)
 
 
 def evaluate_point_estimate(runner, data_loader, net_to_evaluate):

@@ -1,0 +1,76 @@
+"""Independent-chain ensemble across GPUs (one chain per process / GPU).
+
+The reference runs a single chain on a single device (methods/csghmc.py:41).
+Chains are independent Markov chains, so sampling shards with NO
+communication: each rank owns a full chain (theta, v, moments resident in its
+own HBM) keyed by its rank (Philox chain id; seed = base + rank).
+
+The only exchange is at evaluation: the posterior-predictive average over
+chains.  Per batch, each rank holds log p_k(y|x) ([B, C], already averaged over
+its own nst draws as logsumexp(...) - log(nst), methods/sgld.py:300); the
+ensemble predictive is log((1/K) sum_k p_k), one all_reduce(SUM) of
+probabilities over RCCL (backend "nccl" on ROCm; "gloo" on CPU for tests).
+Messages are B x C fp32 (512 KB at B=128, C=1000): latency-bound, far below
+one xGMI link, so no bucketing is needed.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def is_distributed():
+    return dist.is_available() and dist.is_initialized()
+
+
+def world():
+    return dist.get_world_size() if is_distributed() else 1
+
+
+def rank():
+    return dist.get_rank() if is_distributed() else 0
+
+
+def init_chains(backend=None):
+    """Initialise one chain per process from torchrun's env (RANK, WORLD_SIZE,
+    LOCAL_RANK, MASTER_ADDR/PORT).  Returns (rank, world, device)."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if ws > 1 and not is_distributed():
+        backend = backend or ("nccl" if device.type == "cuda" else "gloo")
+        kw = {"device_id": device} if backend == "nccl" else {}
+        dist.init_process_group(backend, **kw)
+    return rank(), world(), device
+
+
+def chain_seed(base_seed):
+    """Per-chain seed: base + rank (each chain its own Philox key)."""
+    return int(base_seed) + rank()
+
+
+def average_predictive(logp):
+    """log((1/K) sum_k exp(logp_k)) over the K chains (one all_reduce)."""
+    k = world()
+    if k == 1:
+        return logp
+    p = logp.float().exp()
+    dist.all_reduce(p, op=dist.ReduceOp.SUM)
+    return (p / k).log()
+
+
+def gather_logits(logits_all):
+    """All-gather per-chain sample logits [B, C, S] into [B, C, S*K] (the
+    reference's logits_all layout with every chain's samples, rank-major)."""
+    k = world()
+    if k == 1:
+        return logits_all
+    parts = [torch.empty_like(logits_all) for _ in range(k)]
+    dist.all_gather(parts, logits_all.contiguous())
+    return torch.cat(parts, dim=2)

@@ -46,10 +46,10 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes
 // Tunables (bdl_set_launch_config).  blocks_per_cu * 256 CUs workgroups, each
 // lane keeps kUnroll float4 groups in flight per iteration.
 // Defaults from the gfx950 sweep (tools/sweep.py, profiles/r01/sweep_*.log):
-// grid-stride with 2 workgroups/CU and 2 float4 groups in flight per lane,
+// grid-stride with 2 workgroups/CU and 1 float4 group in flight per lane,
 // non-temporal 16-B loads and stores, measured best on every kernel kind.
 int g_blocks_per_cu = 2;
-int g_unroll = 2;
+int g_unroll = 1;
 int g_grid_stride = 1;  // 0: one contiguous span per block; 1: grid-stride sweep
 
 int device_cu_count() {
@@ -92,8 +92,10 @@ __device__ __forceinline__ float u01(uint32_t x) {
 }
 
 // Four N(0,1) draws for flat elements 4*group .. 4*group+3.
-__device__ __forceinline__ float4 philox_normal4(uint64_t group, uint64_t seed, uint64_t chain,
-                                                  uint64_t step) {
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4v philox_normal4(uint64_t group, uint64_t seed, uint64_t chain,
+                                               uint64_t step) {
   const uint4 ctr = make_uint4((uint32_t)group, (uint32_t)chain, (uint32_t)step,
                                (uint32_t)(step >> 32));
   const uint4 r = philox4x32_10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
@@ -103,7 +105,7 @@ __device__ __forceinline__ float4 philox_normal4(uint64_t group, uint64_t seed, 
   const float ra = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(r.x)));
   const float rb = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(r.z)));
   const float ta = u01(r.y), tb = u01(r.w);
-  float4 z;
+  f4v z;
   z.x = ra * __builtin_amdgcn_cosf(ta);
   z.y = ra * __builtin_amdgcn_sinf(ta);
   z.z = rb * __builtin_amdgcn_cosf(tb);
@@ -112,11 +114,9 @@ __device__ __forceinline__ float4 philox_normal4(uint64_t group, uint64_t seed, 
 }
 
 // ---------------------------------------------------------------------------
-// Vector helpers: a float4 "group" covers flat elements [4g, 4g+4).  Only the
+// Vector helpers: a 16-B "group" covers flat elements [4g, 4g+4).  Only the
 // very last group of a vector can be partial; it takes the guarded path.
 // ---------------------------------------------------------------------------
-typedef float f4v __attribute__((ext_vector_type(4)));
-
 // 16-B vector access.  Streaming (non-temporal) policy per direction:
 // -DBDL_NT_LOAD / -DBDL_NT_STORE (or -DBDL_NT for both; the default build).
 // Every vector is touched once per step and is far larger than the 256 MiB
@@ -125,17 +125,15 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 #define BDL_NT_LOAD 1
 #define BDL_NT_STORE 1
 #endif
-__device__ __forceinline__ float4 vload(const float* p) {
+__device__ __forceinline__ f4v vload(const float* p) {
 #ifdef BDL_NT_LOAD
-  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+  return __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
 #else
-  const f4v v = *reinterpret_cast<const f4v*>(p);
+  return *reinterpret_cast<const f4v*>(p);
 #endif
-  return make_float4(v.x, v.y, v.z, v.w);
 }
 
-__device__ __forceinline__ void vstore(float* p, float4 x) {
-  const f4v v = {x.x, x.y, x.z, x.w};
+__device__ __forceinline__ void vstore(float* p, f4v v) {
 #ifdef BDL_NT_STORE
   __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
 #else
@@ -143,16 +141,16 @@ __device__ __forceinline__ void vstore(float* p, float4 x) {
 #endif
 }
 
-__device__ __forceinline__ float4 ld4(const float* __restrict__ p, int64_t e, int64_t n) {
+__device__ __forceinline__ f4v ld4(const float* __restrict__ p, int64_t e, int64_t n) {
   if (e + 4 <= n) return vload(p + e);
-  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  f4v v = {0.f, 0.f, 0.f, 0.f};
   if (e + 0 < n) v.x = p[e + 0];
   if (e + 1 < n) v.y = p[e + 1];
   if (e + 2 < n) v.z = p[e + 2];
   return v;
 }
 
-__device__ __forceinline__ void st4(float* __restrict__ p, int64_t e, int64_t n, float4 v) {
+__device__ __forceinline__ void st4(float* __restrict__ p, int64_t e, int64_t n, f4v v) {
   if (e + 4 <= n) {
     vstore(p + e, v);
     return;
@@ -160,23 +158,6 @@ __device__ __forceinline__ void st4(float* __restrict__ p, int64_t e, int64_t n,
   if (e + 0 < n) p[e + 0] = v.x;
   if (e + 1 < n) p[e + 1] = v.y;
   if (e + 2 < n) p[e + 2] = v.z;
-}
-
-__device__ __forceinline__ float& comp(float4& v, int j) {
-  return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
-}
-
-// First run whose end is > idx (runs sorted by end, last end == n).
-__device__ __forceinline__ int find_run(const bdl_run* __restrict__ runs, int nruns, int64_t idx) {
-  int lo = 0, hi = nruns - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (runs[mid].end <= idx)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  return lo;
 }
 
 struct KArgs {
@@ -208,122 +189,303 @@ __device__ __forceinline__ float sdiv(float x, float s, float inv_s) {
 }
 
 // ---------------------------------------------------------------------------
+// Run table staged in LDS (dynamic, 16 B per run, sized per launch).  The fast
+// path reads the block-uniform attribute of its iteration from LDS, so the
+// wait for it is an lgkmcnt wait and never sits behind the data stream's
+// in-order vmcnt.
+// ---------------------------------------------------------------------------
+constexpr int kMaxRuns = 4096;  // 64 KiB of LDS
+
+extern __shared__ bdl_run s_runs[];
+
+__device__ __forceinline__ int64_t run_end(int r) { return s_runs[r].end; }
+__device__ __forceinline__ uint32_t run_attr(int r) { return s_runs[r].attr; }
+
+// First run whose end is > idx.
+__device__ __forceinline__ int find_run_lds(int nruns, int64_t idx) {
+  int lo = 0, hi = nruns - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (run_end(mid) <= idx)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+struct StepConst {
+  bool sgd_mom, sgd_mom_read, has_m2, grad_ready;
+  float inv_s2, inv_nd, inv_ca, inv_cb;
+};
+
+// ---------------------------------------------------------------------------
 // Per-element update.  All arithmetic is separately rounded fp32 in exactly
 // the reference's op order (the file is compiled with -ffp-contract=off).
+// eta / ns are the element's lr and noise scale (its lr group), PRIOR whether
+// the Gaussian-prior term applies, GR = grad already formed (SGD step only).
 // ---------------------------------------------------------------------------
-template <int METHOD, int NOISE, int COLLECT, bool RECIP>
-__device__ __forceinline__ void update_elem(const KArgs& a, uint32_t attr, float& th, float& g,
-                                            float& v, float th0, float eps, float& m1, float& m2,
-                                            float inv_s2, float inv_nd, float inv_ca,
-                                            float inv_cb) {
-  const bool head = (attr & BDL_ATTR_HEAD) != 0;
-  const bool skip = (attr & BDL_ATTR_SKIP) != 0;
-  const float eta = head ? a.lr1 : a.lr0;
-  const float ns = head ? a.ns1 : a.ns0;
-
-  if (!skip && (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) && (a.flags & BDL_FLAG_GRAD_READY)) {
+template <int METHOD, int NOISE, bool RECIP, bool PRIOR, bool GR>
+__device__ __forceinline__ void update_core(const KArgs& a, const StepConst& c, float eta,
+                                            float ns, float& th, float& g, float& v, float th0,
+                                            float eps) {
+  if constexpr (GR) {
     // the sampler gradient was formed (and possibly clipped) by a previous
     // *_GRAD launch: only torch.optim.SGD's step remains
     float stepv = g;
-    if (METHOD == BDL_SGLD && (a.flags & BDL_FLAG_MOMENTUM)) {
+    if (METHOD == BDL_SGLD && c.sgd_mom) {
       v = (a.flags & BDL_FLAG_FIRST_STEP) ? g : (a.mu * v + g);
       stepv = v;
     }
     th = fmaf(-eta, stepv, th);
-  } else if (!skip) {
-    if constexpr (METHOD == BDL_CSGHMC) {
-      // csghmc.py:759-762 — both branches are grad + prior_sig * theta (Q1)
-      const float t = a.prior_sig * th;
-      const float gU = g + t;
-      const float x = v * a.one_minus_alpha;  // :770 v*(1-a)
-      const float y = eta * gU;               //      lr*grad_U
-      float vn = x - y;
-      if constexpr (NOISE != BDL_NOISE_NONE) vn = vn + ns * eps;  // + noise (:765-770)
-      v = vn;                                 // :775
-      th = th + vn;                           // :778 p.data.add_(v)
-    } else if constexpr (METHOD == BDL_SGHMC || METHOD == BDL_SGHMC_GRAD) {
-      float gU = g;  // sghmc.py:494-497
-      if (attr & BDL_ATTR_PRIOR) {
-        const float d = th - th0;
-        const float e = sdiv<RECIP>(d, a.sigma2, inv_s2);
-        gU = g + sdiv<RECIP>(e, a.n_data, inv_nd);
+  } else if constexpr (METHOD == BDL_CSGHMC) {
+    // csghmc.py:759-762 — both branches are grad + prior_sig * theta (Q1)
+    const float t = a.prior_sig * th;
+    const float gU = g + t;
+    const float x = v * a.one_minus_alpha;  // :770 v*(1-a)
+    const float y = eta * gU;               //      lr*grad_U
+    float vn = x - y;
+    if constexpr (NOISE != BDL_NOISE_NONE) vn = vn + ns * eps;  // + noise (:765-770)
+    v = vn;                                 // :775
+    th = th + vn;                           // :778 p.data.add_(v)
+  } else if constexpr (METHOD == BDL_SGHMC || METHOD == BDL_SGHMC_GRAD) {
+    float gU = g;  // sghmc.py:494-497
+    if constexpr (PRIOR) {
+      const float d = th - th0;
+      const float e = sdiv<RECIP>(d, a.sigma2, c.inv_s2);
+      gU = g + sdiv<RECIP>(e, a.n_data, c.inv_nd);
+    }
+    const float s = v * a.one_minus_alpha + eta * gU;  // :504 (two products rounded)
+    const float vn = s + ns * eps;
+    const float gp = g + vn;  // :510 p.grad = p.grad + v
+    v = vn;
+    if constexpr (METHOD == BDL_SGHMC)
+      th = fmaf(-eta, gp, th);  // SGD(momentum=0): param.add_(grad, alpha=-lr)
+    else
+      g = gp;
+  } else {  // BDL_SGLD / BDL_SGLD_GRAD  (sgld.py:471-484)
+    const float nz = ns * eps;
+    float gp;
+    if constexpr (PRIOR) {
+      const float d = th - th0;
+      const float e = sdiv<RECIP>(d, a.sigma2, c.inv_s2);
+      const float f = sdiv<RECIP>(e, a.n_data, c.inv_nd);
+      gp = g + (f + nz);
+    } else {
+      gp = g + nz;
+    }
+    if constexpr (METHOD == BDL_SGLD) {
+      float stepv = gp;
+      if (c.sgd_mom) {  // torch SGD momentum buffer
+        v = (a.flags & BDL_FLAG_FIRST_STEP) ? gp : (a.mu * v + gp);
+        stepv = v;
       }
-      const float s = v * a.one_minus_alpha + eta * gU;  // :504 (two products rounded)
-      const float vn = s + ns * eps;
-      const float gp = g + vn;  // :510 p.grad = p.grad + v
-      v = vn;
-      if constexpr (METHOD == BDL_SGHMC) {
-        th = fmaf(-eta, gp, th);  // SGD(momentum=0): param.add_(grad, alpha=-lr)
-      } else {
-        g = gp;
-      }
-    } else {  // BDL_SGLD / BDL_SGLD_GRAD  (sgld.py:471-484)
-      const float nz = ns * eps;
-      float gp;
-      if (attr & BDL_ATTR_PRIOR) {
-        const float d = th - th0;
-        const float e = sdiv<RECIP>(d, a.sigma2, inv_s2);
-        const float f = sdiv<RECIP>(e, a.n_data, inv_nd);
-        gp = g + (f + nz);
-      } else {
-        gp = g + nz;
-      }
-      if constexpr (METHOD == BDL_SGLD) {
-        float stepv = gp;
-        if (a.flags & BDL_FLAG_MOMENTUM) {  // torch SGD momentum buffer
-          v = (a.flags & BDL_FLAG_FIRST_STEP) ? gp : (a.mu * v + gp);
-          stepv = v;
-        }
-        th = fmaf(-eta, stepv, th);
-      } else {
-        g = gp;
-      }
+      th = fmaf(-eta, stepv, th);
+    } else {
+      g = gp;
     }
   }
+}
 
-  // Posterior moments on the updated theta (parameters_to_vector after step).
+// Posterior moments on the updated theta (parameters_to_vector after step).
+template <int COLLECT, bool RECIP>
+__device__ __forceinline__ void collect_core(const KArgs& a, const StepConst& c, float th,
+                                             float& m1, float& m2) {
   if constexpr (COLLECT == BDL_COLLECT_WELFORD_INIT) {
     m1 = th;
     m2 = 0.0f;
   } else if constexpr (COLLECT == BDL_COLLECT_WELFORD) {
     const float d = th - m1;
-    m1 = m1 + sdiv<RECIP>(d, a.ca, inv_ca);
+    m1 = m1 + sdiv<RECIP>(d, a.ca, c.inv_ca);
     const float d2 = th - m1;
     m2 = m2 + d * d2;
   } else if constexpr (COLLECT == BDL_COLLECT_MEAN_INIT) {
     m1 = th;
     m2 = th * th;
   } else if constexpr (COLLECT == BDL_COLLECT_MEAN) {
-    m1 = sdiv<RECIP>(th + a.ca * m1, a.cb, inv_cb);
-    m2 = sdiv<RECIP>(th * th + a.ca * m2, a.cb, inv_cb);
+    m1 = sdiv<RECIP>(th + a.ca * m1, a.cb, c.inv_cb);
+    m2 = sdiv<RECIP>(th * th + a.ca * m2, a.cb, c.inv_cb);
+  }
+}
+
+// Per-kernel constants of a method / collect combination.
+template <int METHOD, int COLLECT>
+struct StepTraits {
+  static constexpr bool kReadPrior = (METHOD != BDL_CSGHMC);
+  static constexpr bool kMom =
+      (METHOD == BDL_CSGHMC || METHOD == BDL_SGHMC || METHOD == BDL_SGHMC_GRAD);
+  static constexpr bool kWriteTheta =
+      (METHOD == BDL_CSGHMC || METHOD == BDL_SGHMC || METHOD == BDL_SGLD);
+  static constexpr bool kWriteGrad = (METHOD == BDL_SGHMC_GRAD || METHOD == BDL_SGLD_GRAD);
+  static constexpr bool kCollect = (COLLECT != BDL_COLLECT_NONE);
+  static constexpr bool kReadMoments =
+      (COLLECT == BDL_COLLECT_WELFORD || COLLECT == BDL_COLLECT_MEAN);
+};
+
+// FAST PATH: a whole block-iteration (kBlock*UNROLL float4 groups) in range
+// and inside one non-skip run.  eta / ns are scalars, PRIOR / GR compile-time:
+// no branch inside, no bounds checks, every load issued before any arithmetic.
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL, bool PRIOR, bool GR>
+__device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, int64_t gb,
+                                           float eta, float ns) {
+  using T = StepTraits<METHOD, COLLECT>;
+  constexpr bool kPriorLoad = T::kReadPrior && PRIOR && !GR;
+  f4v th[UNROLL], g[UNROLL], v[UNROLL], t0[UNROLL], ep[UNROLL], m1[UNROLL], m2[UNROLL];
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+    v[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
+    th[u] = vload(a.theta + e);
+    g[u] = vload(a.grad + e);
+    if constexpr (T::kMom) v[u] = vload(a.mom + e);
+    if constexpr (METHOD == BDL_SGLD) {
+      if (c.sgd_mom_read) v[u] = vload(a.mom + e);
+    }
+    if constexpr (kPriorLoad) t0[u] = vload(a.prior_mean + e);
+    if constexpr (NOISE == BDL_NOISE_BUFFER && !GR) ep[u] = vload(a.noise + e);
+    if constexpr (T::kReadMoments) {
+      m1[u] = vload(a.mom1 + e);
+      if (c.has_m2) m2[u] = vload(a.mom2 + e);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    const int64_t e = gi * 4;
+    if constexpr (NOISE == BDL_NOISE_PHILOX && !GR)
+      ep[u] = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float xt = th[u][j], xg = g[u][j], xv = v[u][j], x1 = m1[u][j], x2 = m2[u][j];
+      update_core<METHOD, NOISE, RECIP, PRIOR, GR>(a, c, eta, ns, xt, xg, xv, t0[u][j], ep[u][j]);
+      collect_core<COLLECT, RECIP>(a, c, xt, x1, x2);
+      th[u][j] = xt;
+      g[u][j] = xg;
+      v[u][j] = xv;
+      m1[u][j] = x1;
+      m2[u][j] = x2;
+    }
+    if constexpr (T::kWriteTheta) vstore(a.theta + e, th[u]);
+    if constexpr (T::kWriteGrad) vstore(a.grad + e, g[u]);
+    if constexpr (T::kMom) vstore(a.mom + e, v[u]);
+    if constexpr (METHOD == BDL_SGLD) {
+      if (c.sgd_mom) vstore(a.mom + e, v[u]);
+    }
+    if constexpr (T::kCollect) {
+      vstore(a.mom1 + e, m1[u]);
+      if (c.has_m2) vstore(a.mom2 + e, m2[u]);
+    }
+  }
+}
+
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
+__device__ __forceinline__ void chunk_fast_dispatch(const KArgs& a, const StepConst& c,
+                                                    int64_t gb, uint32_t attr) {
+  const bool head = (attr & BDL_ATTR_HEAD) != 0;
+  const float eta = head ? a.lr1 : a.lr0;
+  const float ns = head ? a.ns1 : a.ns0;
+  if constexpr (METHOD == BDL_CSGHMC) {
+    chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(a, c, gb, eta, ns);
+  } else {
+    if constexpr (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) {
+      if (c.grad_ready) {
+        chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, true>(a, c, gb, eta, ns);
+        return;
+      }
+    }
+    if (attr & BDL_ATTR_PRIOR)
+      chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, true, false>(a, c, gb, eta, ns);
+    else
+      chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(a, c, gb, eta, ns);
+  }
+}
+
+// Element-wise update for the slow path: attribute-dependent branches allowed.
+template <int METHOD, int NOISE, int COLLECT, bool RECIP>
+__device__ __forceinline__ void update_elem(const KArgs& a, const StepConst& c, uint32_t attr,
+                                            float& th, float& g, float& v, float th0, float eps,
+                                            float& m1, float& m2) {
+  const bool head = (attr & BDL_ATTR_HEAD) != 0;
+  const float eta = head ? a.lr1 : a.lr0;
+  const float ns = head ? a.ns1 : a.ns0;
+  if (!(attr & BDL_ATTR_SKIP)) {
+    if ((METHOD == BDL_SGLD || METHOD == BDL_SGHMC) && c.grad_ready) {
+      if constexpr (METHOD == BDL_SGLD || METHOD == BDL_SGHMC)
+        update_core<METHOD, NOISE, RECIP, false, true>(a, c, eta, ns, th, g, v, th0, eps);
+    } else if (attr & BDL_ATTR_PRIOR) {
+      update_core<METHOD, NOISE, RECIP, true, false>(a, c, eta, ns, th, g, v, th0, eps);
+    } else {
+      update_core<METHOD, NOISE, RECIP, false, false>(a, c, eta, ns, th, g, v, th0, eps);
+    }
+  }
+  collect_core<COLLECT, RECIP>(a, c, th, m1, m2);
+}
+
+// SLOW PATH: an iteration that reaches the end of the vector / span, crosses a
+// run boundary or covers a skipped parameter.  Per-lane predicates, guarded
+// partial groups, a per-element run search (in LDS).  Taken for
+// O(#runs + #blocks) iterations per launch.
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
+__device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, int64_t gb,
+                                           int64_t gend) {
+  using T = StepTraits<METHOD, COLLECT>;
+  const int64_t n = a.n;
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    if (gi >= gend) continue;
+    const int64_t e = gi * 4;
+    const f4v z = {0.f, 0.f, 0.f, 0.f};
+    f4v th = ld4(a.theta, e, n), g = ld4(a.grad, e, n), v = z, t0 = z, ep = z, m1 = z, m2 = z;
+    if (T::kMom || (METHOD == BDL_SGLD && c.sgd_mom_read)) v = ld4(a.mom, e, n);
+    if (T::kReadPrior) t0 = ld4(a.prior_mean, e, n);
+    if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, n);
+    if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+    if (T::kReadMoments) {
+      m1 = ld4(a.mom1, e, n);
+      if (c.has_m2) m2 = ld4(a.mom2, e, n);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (e + j >= n) break;
+      const uint32_t at = run_attr(find_run_lds(a.nruns, e + j));
+      float xt = th[j], xg = g[j], xv = v[j], x1 = m1[j], x2 = m2[j];
+      update_elem<METHOD, NOISE, COLLECT, RECIP>(a, c, at, xt, xg, xv, t0[j], ep[j], x1, x2);
+      th[j] = xt;
+      g[j] = xg;
+      v[j] = xv;
+      m1[j] = x1;
+      m2[j] = x2;
+    }
+    if (T::kWriteTheta) st4(a.theta, e, n, th);
+    if (T::kWriteGrad) st4(a.grad, e, n, g);
+    if (T::kMom || (METHOD == BDL_SGLD && c.sgd_mom)) st4(a.mom, e, n, v);
+    if (T::kCollect) {
+      st4(a.mom1, e, n, m1);
+      if (c.has_m2) st4(a.mom2, e, n, m2);
+    }
   }
 }
 
 template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
 __device__ __forceinline__ void step_body(const KArgs& a) {
-  constexpr bool kReadPrior = (METHOD != BDL_CSGHMC);
-  constexpr bool kMom =
-      (METHOD == BDL_CSGHMC || METHOD == BDL_SGHMC || METHOD == BDL_SGHMC_GRAD);
-  constexpr bool kWriteTheta = (METHOD == BDL_CSGHMC || METHOD == BDL_SGHMC || METHOD == BDL_SGLD);
-  constexpr bool kWriteGrad = (METHOD == BDL_SGHMC_GRAD || METHOD == BDL_SGLD_GRAD);
-  constexpr bool kCollect = (COLLECT != BDL_COLLECT_NONE);
-  constexpr bool kReadMoments = (COLLECT == BDL_COLLECT_WELFORD || COLLECT == BDL_COLLECT_MEAN);
+  StepConst c;
+  c.sgd_mom = (METHOD == BDL_SGLD) && (a.flags & BDL_FLAG_MOMENTUM);
+  c.sgd_mom_read = c.sgd_mom && !(a.flags & BDL_FLAG_FIRST_STEP);
+  c.has_m2 = (COLLECT != BDL_COLLECT_NONE) && (a.mom2 != nullptr);
+  c.grad_ready = (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) && (a.flags & BDL_FLAG_GRAD_READY);
+  c.inv_s2 = 1.0f / a.sigma2;
+  c.inv_nd = 1.0f / a.n_data;
+  c.inv_ca = 1.0f / a.ca;
+  c.inv_cb = 1.0f / a.cb;
 
-  const bool sgd_mom = (METHOD == BDL_SGLD) && (a.flags & BDL_FLAG_MOMENTUM);
-  const bool sgd_mom_read = sgd_mom && !(a.flags & BDL_FLAG_FIRST_STEP);
-  const bool has_m2 = kCollect && (a.mom2 != nullptr);
-
-  const float inv_s2 = 1.0f / a.sigma2;
-  const float inv_nd = 1.0f / a.n_data;
-  const float inv_ca = 1.0f / a.ca;
-  const float inv_cb = 1.0f / a.cb;
-
-  const int64_t n = a.n;
-  const int64_t ngroups = (n + 3) >> 2;
+  const int64_t ngroups = (a.n + 3) >> 2;
+  const int64_t nfull = a.n >> 2;  // groups entirely inside [0, n)
   // Two sweep orders: each block owns one contiguous span (groups_per_block >
   // 0), or all blocks advance through the vector together (grid-stride,
-  // groups_per_block == 0).  Either way a lane's groups only move forward, so
-  // its run cursor advances monotonically.
+  // groups_per_block == 0).  Either way the block's iterations only move
+  // forward, so its (block-uniform) run cursor advances monotonically.
   constexpr int64_t kIter = (int64_t)kBlock * UNROLL;
   int64_t g0, g1, gstep;
   if (a.groups_per_block > 0) {
@@ -335,77 +497,22 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
     g1 = ngroups;
     gstep = (int64_t)gridDim.x * kIter;
   }
+
+  // stage the run table in LDS
+  for (int i = threadIdx.x; i < a.nruns; i += kBlock) s_runs[i] = a.runs[i];
+  __syncthreads();
   if (g0 >= g1) return;
 
-  // Block-uniform run search for the span start; each lane then advances.
-  int r = find_run(a.runs, a.nruns, g0 * 4);
-  int64_t run_hi = a.runs[r].end;
-  uint32_t run_attr = a.runs[r].attr;
-
+  int r = find_run_lds(a.nruns, g0 * 4);
   for (int64_t gb = g0; gb < g1; gb += gstep) {
-    float4 th[UNROLL], g[UNROLL], v[UNROLL], t0[UNROLL], ep[UNROLL], m1[UNROLL], m2[UNROLL];
-    int64_t e[UNROLL];
-    bool act[UNROLL];
-
-    // ---- issue every load of this iteration before any arithmetic ----
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
-      act[u] = gi < g1;
-      e[u] = gi * 4;
-      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-      th[u] = g[u] = v[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
-      if (act[u]) {
-        th[u] = ld4(a.theta, e[u], n);
-        g[u] = ld4(a.grad, e[u], n);
-        if (kMom || sgd_mom_read) v[u] = ld4(a.mom, e[u], n);
-        if (kReadPrior) t0[u] = ld4(a.prior_mean, e[u], n);
-        if (NOISE == BDL_NOISE_BUFFER) ep[u] = ld4(a.noise, e[u], n);
-        if (kReadMoments) {
-          m1[u] = ld4(a.mom1, e[u], n);
-          if (has_m2) m2[u] = ld4(a.mom2, e[u], n);
-        }
-      }
-    }
-
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      if (!act[u]) continue;
-      if constexpr (NOISE == BDL_NOISE_PHILOX)
-        ep[u] = philox_normal4((uint64_t)(e[u] >> 2), a.seed, a.chain, a.step);
-
-      // attributes: fast path when the whole group sits in the cursor's run
-      while (run_hi <= e[u] && r < a.nruns - 1) {
-        ++r;
-        run_hi = a.runs[r].end;
-        run_attr = a.runs[r].attr;
-      }
-      uint32_t at[4] = {run_attr, run_attr, run_attr, run_attr};
-      if (e[u] + 4 > run_hi) {  // group straddles a run boundary (rare)
-        int rr = r;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          while (rr < a.nruns - 1 && a.runs[rr].end <= e[u] + j) ++rr;
-          at[j] = a.runs[rr].attr;
-        }
-      }
-
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        update_elem<METHOD, NOISE, COLLECT, RECIP>(a, at[j], comp(th[u], j), comp(g[u], j),
-                                                   comp(v[u], j), comp(t0[u], j), comp(ep[u], j),
-                                                   comp(m1[u], j), comp(m2[u], j), inv_s2, inv_nd,
-                                                   inv_ca, inv_cb);
-      }
-
-      if (kWriteTheta) st4(a.theta, e[u], n, th[u]);
-      if (kWriteGrad) st4(a.grad, e[u], n, g[u]);
-      if (kMom || sgd_mom) st4(a.mom, e[u], n, v[u]);
-      if (kCollect) {
-        st4(a.mom1, e[u], n, m1[u]);
-        if (has_m2) st4(a.mom2, e[u], n, m2[u]);
-      }
-    }
+    while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
+    const int64_t gend = min(gb + kIter, g1);
+    const uint32_t attr = run_attr(r);
+    if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 &&
+        !(attr & BDL_ATTR_SKIP))
+      chunk_fast_dispatch<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, attr);
+    else
+      chunk_slow<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, gend);
   }
 }
 
@@ -436,16 +543,16 @@ __global__ __launch_bounds__(kBlock) void bdl_moments_kernel(const MArgs a) {
   for (int64_t gi = (int64_t)blockIdx.x * kBlock + threadIdx.x; gi < ngroups;
        gi += (int64_t)gridDim.x * kBlock) {
     const int64_t e = gi * 4;
-    float4 t = ld4(a.theta, e, a.n), m1 = make_float4(0, 0, 0, 0), m2 = m1;
+    const f4v t = ld4(a.theta, e, a.n);
+    f4v m1 = {0.f, 0.f, 0.f, 0.f}, m2 = m1;
     if (a.collect == BDL_COLLECT_WELFORD || a.collect == BDL_COLLECT_MEAN) {
       m1 = ld4(a.mom1, e, a.n);
       if (a.mom2) m2 = ld4(a.mom2, e, a.n);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float x = comp(t, j);
-      float& p = comp(m1, j);
-      float& q = comp(m2, j);
+      const float x = t[j];
+      float p = m1[j], q = m2[j];
       switch (a.collect) {
         case BDL_COLLECT_WELFORD_INIT:
           p = x;
@@ -469,6 +576,8 @@ __global__ __launch_bounds__(kBlock) void bdl_moments_kernel(const MArgs a) {
           q = a.recip ? w * inv_cb : w / a.cb;
         }
       }
+      m1[j] = p;
+      m2[j] = q;
     }
     st4(a.mom1, e, a.n, m1);
     if (a.mom2) st4(a.mom2, e, a.n, m2);
@@ -491,17 +600,17 @@ __global__ __launch_bounds__(kBlock) void bdl_sample_kernel(const SArgs a) {
   for (int64_t gi = (int64_t)blockIdx.x * kBlock + threadIdx.x; gi < ngroups;
        gi += (int64_t)gridDim.x * kBlock) {
     const int64_t e = gi * 4;
-    const float4 m = ld4(a.mom1, e, a.n);
-    float4 q = make_float4(0, 0, 0, 0);
+    const f4v m = ld4(a.mom1, e, a.n);
+    f4v q = {0.f, 0.f, 0.f, 0.f};
     if (a.mom2) q = ld4(a.mom2, e, a.n);
-    float4 eps = (a.noise_mode == BDL_NOISE_BUFFER) ? ld4(a.noise, e, a.n)
-                                                    : philox_normal4((uint64_t)gi, a.seed, a.chain,
-                                                                     a.step);
-    float4 o;
+    const f4v eps = (a.noise_mode == BDL_NOISE_BUFFER)
+                        ? ld4(a.noise, e, a.n)
+                        : philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+    f4v o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float mj = comp(const_cast<float4&>(m), j);
-      const float qj = comp(q, j);
+      const float mj = m[j];
+      const float qj = q[j];
       float var;
       if (!a.mom2)
         var = a.var_floor;  // single-sample cycle: ones*1e-12 (csghmc.py:456-458)
@@ -512,7 +621,7 @@ __global__ __launch_bounds__(kBlock) void bdl_sample_kernel(const SArgs a) {
       else
         var = qj;
       if (!(var != var)) var = fmaxf(var, a.var_floor);  // clamp_(min=1e-12); NaN stays NaN
-      comp(o, j) = mj + sqrtf(var) * comp(eps, j);  // p_m + p_v.sqrt()*eps
+      o[j] = mj + sqrtf(var) * eps[j];  // p_m + p_v.sqrt()*eps
     }
     st4(a.out, e, a.n, o);
   }
@@ -617,7 +726,7 @@ const char* bdl_last_error(void) { return g_last_error.c_str(); }
 int bdl_set_launch_config(int32_t blocks_per_cu, int32_t unroll, int32_t grid_stride) {
   const int prev = (g_grid_stride << 24) | (g_blocks_per_cu << 8) | g_unroll;
   g_blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : 2;
-  g_unroll = (unroll == 1 || unroll == 2 || unroll == 4) ? unroll : 2;
+  g_unroll = (unroll == 1 || unroll == 2 || unroll == 4) ? unroll : 1;
   g_grid_stride = grid_stride > 0 ? 1 : 0;
   return prev;
 }
@@ -676,6 +785,8 @@ int bdl_sgmcmc_step(const bdl_step_args* s, void* stream) {
   const bool needs_prior = s->method != BDL_CSGHMC;
   if (!s->theta || !s->grad || !s->runs || s->nruns < 1)
     return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: theta, grad and runs are required");
+  if (s->nruns > kMaxRuns)
+    return fail(BDL_ERR_RUNS, "bdl_sgmcmc_step: more than 4096 runs (merge parameter groups)");
   if (needs_mom && !s->mom) return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: mom is required");
   if (needs_prior && !s->prior_mean)
     return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: prior_mean is required for sghmc/sgld");
@@ -729,7 +840,8 @@ int bdl_sgmcmc_step(const bdl_step_args* s, void* stream) {
   a.chain = s->chain;
   a.step = s->step;
 
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kBlock), (size_t)s->nruns * sizeof(bdl_run),
+                     (hipStream_t)stream, a);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     g_last_error = std::string("bdl_sgmcmc_step: launch failed: ") + hipGetErrorString(err);

@@ -102,3 +102,45 @@ def philox_normal(n, seed, chain, step, device="cuda"):
 
 def set_launch_config(blocks_per_cu=0, unroll=0, grid_stride=0):
     return L.lib().bdl_set_launch_config(int(blocks_per_cu), int(unroll), int(grid_stride))
+
+
+# Launch geometries worth trying on gfx950 (workgroups/CU, float4 groups in
+# flight per lane, grid-stride): the sweep (profiles/r01) shows the optimum
+# moving between these from one device to the next.
+AUTOTUNE_CANDIDATES = ((2, 1, 1), (1, 4, 1), (3, 1, 1), (2, 4, 1), (1, 2, 1))
+
+
+def autotune(n, device=None, reps=6, candidates=AUTOTUNE_CANDIDATES):
+    """Pick the fastest launch geometry for an n-element sweep on this device.
+
+    The update of every element is independent of the launch geometry (noise
+    is keyed by element index), so the choice changes speed only, never
+    results.  Times the cSGHMC exploration kernel on scratch buffers (3 x n
+    fp32, freed afterwards) and installs the winner process-wide.  Returns
+    (config, {config: ms})."""
+    import numpy as np
+
+    from .flat import FlatState
+    dev = torch.device(device) if device is not None else torch.device("cuda",
+                                                                        torch.cuda.current_device())
+    st = FlatState.from_segments([("w", (int(n),))], None, device=dev)
+    st.theta.zero_()
+    kw = dict(lrs=(1e-4, 1e-4), noise_scale=(0.0, 0.0), noise_mode=L.NOISE_NONE,
+              one_minus_alpha=0.9, prior_sig=1.0)
+    times = {}
+    for cfg in candidates:
+        set_launch_config(*cfg)
+        for _ in range(2):
+            sgmcmc_step(st, L.CSGHMC, **kw)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(reps)]
+        for e0, e1 in ev:
+            e0.record()
+            sgmcmc_step(st, L.CSGHMC, **kw)
+            e1.record()
+        torch.cuda.synchronize(dev)
+        times[cfg] = float(np.median([a.elapsed_time(b) for a, b in ev]))
+    best = min(times, key=times.get)
+    set_launch_config(*best)
+    del st
+    return best, times

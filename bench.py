@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--blocks-per-cu", type=int, default=0)
     ap.add_argument("--unroll", type=int, default=0)
     ap.add_argument("--grid-stride", type=int, default=-1)
+    ap.add_argument("--no-autotune", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -110,9 +111,21 @@ def main():
     from bayesdll_amd.flat import FlatState
     from bayesdll_amd.shapes import segments
 
+    segs, readout = segments(a.backbone, a.num_classes)
+    tuned = None
     if a.blocks_per_cu or a.unroll or a.grid_stride >= 0:
         K.set_launch_config(a.blocks_per_cu, a.unroll, max(a.grid_stride, 0))
-    segs, readout = segments(a.backbone, a.num_classes)
+        launch = {"blocks_per_cu": a.blocks_per_cu, "unroll": a.unroll,
+                  "grid_stride": max(a.grid_stride, 0), "autotuned": False}
+    elif not a.no_autotune:
+        # untimed setup (like cudnn.benchmark): pick the launch geometry for
+        # this device; results are identical under every geometry
+        best, tuned = K.autotune(sum(int(np.prod(s)) for _, s in segs), device=local)
+        launch = {"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
+                  "autotuned": True,
+                  "candidates_ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4) for c, t in tuned.items()}}
+    else:
+        launch = {"default": True, "autotuned": False}
     dev = torch.device("cuda", local)
     st = FlatState.from_segments(segs, readout, device=dev)
     gen = torch.Generator(device=dev).manual_seed(42 + rank)
@@ -229,6 +242,7 @@ def main():
                    "cycles": a.cycles, "thin": a.thin, "beta": 0.5, "noise": "philox",
                    "parallelism": f"{world} independent chains (1/GPU)"},
         "hbm_gbs": round(hbm_gbs * world, 1),
+        "launch": launch,
         "kernels": table,
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
