@@ -1,0 +1,66 @@
+"""Summarise a tools/profile.sh run (gpurun_out/prof_<tag>) into profiles/<tag>/.
+
+* kernel stats (rocprofv3 --kernel-trace --stats) copied as-is;
+* FETCH_SIZE / WRITE_SIZE per dispatch of the fused step kernels (separate
+  PMC passes), reduced to mean HBM bytes per launch per kernel kind, with the
+  gfx950 correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE reports half of a
+  16-B/lane streaming read, so bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024;
+* profiles/pmc_traffic.json updated (read by bench.py for roofline.traffic).
+
+usage: python tools/pmc_summary.py <tag>
+"""
+import csv
+import json
+import os
+import re
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KIND = {(0, 0): "explore", (2, 0): "sample", (2, 1): "collect_init", (2, 2): "collect"}
+
+
+def kind_of(name):
+    m = re.search(r"bdl_step_kernel<(\d+), (\d+), (\d+), (\d+)>", name)
+    if not m or int(m.group(1)) != 0:
+        return None
+    return KIND.get((int(m.group(2)), int(m.group(3))))
+
+
+def main(tag):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
+                os.path.join(dst, "bench_kernel_stats.csv"))
+    acc = {}
+    for sub, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        rows = [r for r in csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv")))
+                if "bdl_step_kernel" in r["Kernel_Name"]]
+        with open(os.path.join(dst, f"pmc_{sub}.csv"), "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Counter_Name",
+                                              "Counter_Value", "VGPR_Count", "SGPR_Count",
+                                              "Grid_Size", "LDS_Block_Size"],
+                               extrasaction="ignore")
+            w.writeheader()
+            for r in rows:
+                w.writerow(r)
+                k = kind_of(r["Kernel_Name"])
+                if k:
+                    acc.setdefault(k, {}).setdefault(counter, []).append(float(r["Counter_Value"]))
+    traffic, raw = {}, {}
+    for k, d in acc.items():
+        raw[k] = {c: sum(v) / len(v) for c, v in d.items()}
+        if "FETCH_SIZE" in raw[k] and "WRITE_SIZE" in raw[k]:
+            traffic[k] = int((2 * raw[k]["FETCH_SIZE"] + raw[k]["WRITE_SIZE"]) * 1024)
+    out = {"vit_l_32": traffic, "_source": f"profiles/{tag}",
+           "_method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; bytes "
+                      "per launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE "
+                      "reports half of a 16-B/lane streaming read, MI355X_MICROARCH.md)",
+           "_raw_kib_per_launch": raw}
+    json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
