@@ -33,7 +33,7 @@ EVAL_STEP_BASE = 1 << 62  # Philox step keys for evaluation draws (never used by
 class PosteriorDraw:
     """An evaluation copy of `net` whose flat theta the sample kernel fills."""
 
-    def __init__(self, net, noise_mode, seed, chain):
+    def __init__(self, net, noise_mode, seed, chain, provider=None):
         self.net = copy.deepcopy(net)
         for p in self.net.parameters():
             p.grad = None
@@ -44,6 +44,9 @@ class PosteriorDraw:
         self.chain = chain
         self.count = 0
         self.noise = None if noise_mode == "philox" else torch.empty_like(self.theta)
+        self.provider = provider
+        if noise_mode == "external" and provider is None:
+            raise RuntimeError("noise_mode='external' needs Model.noise_provider")
 
     def load_mean(self, mean):
         self.theta.copy_(mean)
@@ -51,8 +54,11 @@ class PosteriorDraw:
     def draw(self, mean, m2, var_mode, ratio):
         """theta = mean + sqrt(clamp(var, 1e-12)) * eps; m2=None -> var = 1e-12."""
         noise = None
-        if self.noise_mode != "philox":
+        if self.noise_mode == "torch":
             noise = fill_normal_per_tensor(self.noise, self.numels)
+        elif self.noise_mode == "external":
+            self.provider(-1 - self.count, self.noise)
+            noise = self.noise
         K.posterior_sample(self.theta, mean, m2, var_mode=var_mode, ratio=ratio, noise=noise,
                            seed=self.seed, chain=self.chain, step=EVAL_STEP_BASE + self.count)
         self.count += 1
@@ -113,7 +119,8 @@ def mixture_evaluate(runner, test_loader, var_of_cycle):
     weights = runner.calculate_gmm_weights()
     runner.logger.info(f"GMM component weights: {weights}")
     model = runner.model
-    draw = PosteriorDraw(runner.net, model.noise_mode, model.seed, model.chain)
+    draw = PosteriorDraw(runner.net, model.noise_mode, model.seed, model.chain,
+                         model.noise_provider)
     loss, error, nb = 0.0, 0, 0
     targets, logits, logits_all = [], [], []
     draw.net.eval()
@@ -165,7 +172,8 @@ def sample_average_evaluate(runner, test_loader, mean, m2, var_mode, ratio):
     (methods/sgld.py:253-321), across chains via chain_average_logprob."""
     args = runner.args
     model = runner.model
-    draw = PosteriorDraw(runner.net, model.noise_mode, model.seed, model.chain)
+    draw = PosteriorDraw(runner.net, model.noise_mode, model.seed, model.chain,
+                         model.noise_provider)
     draw.net.eval()
     loss, error, nb = 0.0, 0, 0
     targets, logits, logits_all = [], [], []

@@ -256,7 +256,8 @@ class Runner:
         mean = self.cycle_theta_mom1[c]
         m2, var_mode, ratio = self._variance_source(c)
         model = self.model
-        draw = R.PosteriorDraw(self.net, model.noise_mode, model.seed, model.chain)
+        draw = R.PosteriorDraw(self.net, model.noise_mode, model.seed, model.chain,
+                               model.noise_provider)
         likelihoods = []
         for sample_idx in range(max(1, self.nst)):
             if self.nst > 0:

@@ -224,7 +224,8 @@ class Runner:
         mean = self.cycle_theta_mom1[c]
         m2, mode, ratio = self._variance_source(c)
         model = self.model
-        draw = R.PosteriorDraw(self.net, model.noise_mode, model.seed, model.chain)
+        draw = R.PosteriorDraw(self.net, model.noise_mode, model.seed, model.chain,
+                               model.noise_provider)
         out = []
         for _ in range(max(1, self.nst)):
             if self.nst > 0:

@@ -112,3 +112,36 @@ def fake_loader(batches: int, batch_size: int = 4, device="cpu"):
     x = torch.zeros(batch_size, 1, device=device)
     y = torch.zeros(batch_size, dtype=torch.long, device=device)
     return [(x, y) for _ in range(batches)]
+
+
+class MLP(nn.Module):
+    """mlp_mnist backbone with the reference's parameter names and shapes
+    (networks/small_nets.py MLP(784, 10, width=1000, depth=3), readout
+    'classifier'); written here so the GPU tests need no reference import."""
+
+    def __init__(self, input_dim=784, output_dim=10, width=1000, depth=3):
+        super().__init__()
+        self.input_dim = input_dim
+        layers, hin = [], input_dim
+        for _ in range(depth):
+            layers += [nn.Linear(hin, width), nn.ReLU()]
+            hin = width
+        self.layers = nn.Sequential(*layers)
+        self.classifier = nn.Linear(width, output_dim)
+        self.readout_name = "classifier"
+
+    def forward(self, x):
+        return self.classifier(self.layers(x.view(-1, self.input_dim)))
+
+
+def det_normal(seed, k, numel):
+    """Deterministic N(0,1) stream replacing torch.randn_like draw #k."""
+    rng = np.random.default_rng([int(seed), 0xD4A7, int(k)])
+    return rng.standard_normal(int(numel), dtype=np.float32)
+
+
+def synthetic_mnist(seed, n, batch, device="cpu"):
+    rng = np.random.default_rng([int(seed), 0xDA7A])
+    x = torch.from_numpy(rng.standard_normal((n, 1, 28, 28), dtype=np.float32))
+    y = torch.from_numpy(rng.integers(0, 10, size=n).astype(np.int64))
+    return [(x[i:i + batch].to(device), y[i:i + batch].to(device)) for i in range(0, n, batch)]

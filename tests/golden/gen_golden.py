@@ -34,8 +34,8 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))  # tests/ for fakenet
-from fakenet import (TOY_SEGMENTS, TOY_READOUT, FakeNet, fake_loader, init_vector,  # noqa: E402
-                     numel_of)
+from fakenet import (TOY_SEGMENTS, TOY_READOUT, FakeNet, det_normal, fake_loader,  # noqa: E402
+                     init_vector, numel_of, synthetic_mnist)
 
 REF = "/root/reference"
 
@@ -264,11 +264,120 @@ def schedule_tables(methods):
     return out
 
 
+# --------------------------------------------------------------------------
+# Runner.train() end to end on the reference's real mlp_mnist backbone
+# (networks/small_nets.py), synthetic MNIST-shaped data (config 1 / 2).  The
+# torch.randn_like stream is replaced by a deterministic numpy stream
+# (fakenet.det_normal, draw counter k) so the product can replay it on the GPU
+# without storing 2.8M-element draws; the draw ORDER is pinned by the
+# FakeNet fixtures above, which capture torch's own stream.
+# --------------------------------------------------------------------------
+MLP_CONFIGS = {
+    # config 2: mlp_mnist cSGHMC (hparams of pretrain_resnet101.py:127)
+    "mlp_csghmc_c2": ("csghmc", dict(epochs=4, ntrain=512, ntest=256, batch=128, num_cycles=2,
+                                     beta=0.5, lr=0.02, lr_head=0.02, ND=30000, data_seed=1,
+                                     init_seed=2, noise_seed=3,
+                                     hparams=dict(prior_sig=1.0, bias="informative",
+                                                  momentum_decay=0.18, Ninflate=1.0, nd=0.01,
+                                                  burnin=0, thin=1, nst=2))),
+    # config 1: mlp_mnist SGLD (README.md:83 hparams; burnin/epochs shortened)
+    "mlp_sgld_c1": ("sgld", dict(epochs=3, ntrain=512, ntest=256, batch=128, lr=1e-2,
+                                 lr_head=1e-2, momentum=0.5, ND=30000, data_seed=4, init_seed=5,
+                                 noise_seed=6,
+                                 hparams=dict(prior_sig=1.0, bias="informative", Ninflate=1e3,
+                                              nd=1.0, burnin=1, thin=2, nst=2))),
+}
+SUBSET = 4096
+
+
+def subset_idx(n, seed=99):
+    return np.sort(np.random.default_rng(seed).choice(n, size=SUBSET, replace=False))
+
+
+def run_mlp(methods, method, cfg):
+    from networks import small_nets
+    torch.manual_seed(0)
+    net = small_nets.MLP(input_dim=784, output_dim=10, width=1000, depth=3)
+    net.readout_name = "classifier"
+    n = sum(p.numel() for p in net.parameters())
+    theta0 = init_vector(cfg["init_seed"], n, 0.03)
+    with torch.no_grad():
+        torch.nn.utils.vector_to_parameters(torch.tensor(theta0), net.parameters())
+    train = synthetic_mnist(cfg["data_seed"], cfg["ntrain"], cfg["batch"])
+    test = synthetic_mnist(cfg["data_seed"] + 100, cfg["ntest"], cfg["batch"])
+    tmp = tempfile.mkdtemp(prefix="bdl_golden_mlp_")
+    args = make_args(tmp, epochs=cfg["epochs"], num_cycles=cfg.get("num_cycles", 2), lr=cfg["lr"],
+                     lr_head=cfg["lr_head"], momentum=cfg.get("momentum", 0.0), ND=cfg["ND"],
+                     proportion_exploration=cfg.get("beta", 0.5), test_eval_freq=1,
+                     hparams={k: str(v) for k, v in cfg["hparams"].items()})
+    mod = getattr(methods, method)
+    runner = mod.Runner(net, None, args, logging.getLogger("golden"))
+    counter = [0]
+    orig = torch.randn_like
+
+    def det_randn_like(t, *a, **k):
+        out = torch.from_numpy(det_normal(cfg["noise_seed"], counter[0], t.numel())).reshape(t.shape)
+        counter[0] += 1
+        return out.to(t.dtype)
+
+    evals = []
+    orig_eval = mod.Runner.evaluate
+
+    def ev(self, loader):
+        r = orig_eval(self, loader)
+        evals.append(r)
+        return r
+
+    torch.randn_like = det_randn_like
+    mod.Runner.evaluate = ev
+    try:
+        res = runner.train(train, None, test)
+    finally:
+        torch.randn_like = orig
+        mod.Runner.evaluate = orig_eval
+    idx = subset_idx(n)
+    theta = torch.nn.utils.parameters_to_vector(runner.net.parameters()).detach().numpy()
+    out = dict(config=json.dumps(dict(cfg, method=method)), idx=idx, theta_sub=theta[idx],
+               theta_norm=np.float64(np.linalg.norm(theta.astype(np.float64))),
+               draws=np.int64(counter[0]))
+    if res is not None:
+        out["losses_train"] = res["losses_train"]
+        out["errors_train"] = res["errors_train"]
+        out["losses_test"] = res["losses_test"]
+        out["errors_test"] = res["errors_test"]
+    last = evals[-1]
+    out["eval_loss"] = np.float64(last[0])
+    out["eval_err"] = np.float64(last[1])
+    out["eval_logits"] = last[3].astype(np.float32)
+    out["n_evals"] = np.int64(len(evals))
+    if method in ("csghmc", "csgld"):
+        cyc = sorted(runner.cycle_theta_mom1.keys())
+        out["cycles"] = np.array(cyc)
+        out["samples_per_cycle"] = np.array([runner.samples_per_cycle[c] for c in cyc])
+        out["cycle_mom1_sub"] = np.stack([runner.cycle_theta_mom1[c].numpy()[idx] for c in cyc])
+        out["cycle_mom2_sub"] = np.stack([runner.cycle_theta_mom2[c].numpy()[idx] for c in cyc])
+        out["cycle_likelihoods"] = np.stack([np.asarray(runner.cycle_likelihoods[c])
+                                             for c in sorted(runner.cycle_likelihoods)])
+    else:
+        out["post_mom1_sub"] = runner.post_theta_mom1.numpy()[idx]
+        out["post_mom2_sub"] = runner.post_theta_mom2.numpy()[idx]
+        out["post_cnt"] = np.int64(runner.post_theta_cnt)
+    return out
+
+
 def main():
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
     logging.basicConfig(level=logging.WARNING)
     methods = import_reference()
     torch.set_num_threads(1)
+    only = os.environ.get("GOLDEN_ONLY")
+    if only == "mlp":
+        torch.set_num_threads(8)
+        for name, (method, cfg) in MLP_CONFIGS.items():
+            rec = run_mlp(methods, method, copy.deepcopy(cfg))
+            np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **rec)
+            print(f"wrote {name}.npz draws={int(rec['draws'])} evals={int(rec['n_evals'])}")
+        return
     for name, (method, cfg) in CONFIGS.items():
         rec = run_method(methods, method, copy.deepcopy(cfg))
         path = os.path.join(HERE, f"{name}.npz")

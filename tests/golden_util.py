@@ -15,8 +15,9 @@ def load(name):
     d = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     out = {k: d[k] for k in d.files}
     out["config"] = json.loads(str(out["config"]))
-    out["segments"] = [(nm, tuple(s)) for nm, s in json.loads(str(out["segments"]))]
-    out["readout"] = str(out["readout"])
+    if "segments" in out:
+        out["segments"] = [(nm, tuple(s)) for nm, s in json.loads(str(out["segments"]))]
+        out["readout"] = str(out["readout"])
     return out
 
 
