@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--unroll", type=int, default=0)
     ap.add_argument("--grid-stride", type=int, default=-1)
     ap.add_argument("--no-autotune", action="store_true")
+    ap.add_argument("--e2e-steps", type=int, default=10)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -100,6 +101,37 @@ def cpu_baseline(segs, readout, seconds):
     return {"value": steps / el, "unit": "steps/s", "cores": threads, "kind": "port",
             "sample": f"{steps} full ViT-L/32 cSGHMC updates (296 tensors, 306,535,400 params, "
                       f"randn_like noise) in {el:.1f} s on {cpu_model}"}
+
+
+def e2e_steps(steps, warmup, local, seed):
+    """Informational: full cSGHMC steps on a real ViT-L/32 (random init,
+    synthetic [16,3,224,224] batch): forward + backward (PyTorch-ROCm fp32
+    autograd, gradients written into the flat buffer) + the fused update.
+    Returns ms/step and the fused kernel's share."""
+    import bayesdll_amd.csghmc as csghmc
+    from bayesdll_amd.backbones import backbone
+    dev = torch.device("cuda", local)
+    torch.manual_seed(seed)
+    net = backbone("vit_l_32", 1000).to(dev)
+    model = csghmc.Model(ND=1840, prior_sig=1.0, momentum_decay=0.18)
+    model.noise_mode = "philox"
+    crit = torch.nn.CrossEntropyLoss()
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = torch.randn(16, 3, 224, 224, device=dev, generator=g)
+    y = torch.randint(0, 1000, (16,), device=dev, generator=g)
+    for k in range(warmup):
+        model(x, y, net, None, crit, [1e-4, 1e-2], 1.0, 0.01, should_sample=(k % 2 == 0))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        model(x, y, net, None, crit, [1e-4, 1e-2], 1.0, 0.01, should_sample=(k % 10 == 0))
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    del net, model
+    torch.cuda.empty_cache()
+    return {"steps_per_s": round(1e3 / ms, 2), "ms_per_step": round(ms, 3),
+            "batch": [16, 3, 224, 224], "what": "ViT-L/32 fp32 fwd+bwd (autograd) + fused cSGHMC "
+            "update, loss.item() sync per step as in the reference (informational)"}
 
 
 def main():
@@ -249,6 +281,12 @@ def main():
                      "traffic": traffic,
                      "alg_bytes_per_launch": alg_bytes},
     }
+    if world == 1 and a.e2e_steps > 0 and a.backbone == "vit_l_32":
+        del st, m1s, m2s
+        torch.cuda.empty_cache()
+        e2e = e2e_steps(a.e2e_steps, 3, local, 42)
+        e2e["fused_update_share"] = round(dom["avg_ms"] / e2e["ms_per_step"], 4)
+        out["e2e"] = e2e
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(segs, readout, a.cpu_baseline_seconds)
     if rank == 0:

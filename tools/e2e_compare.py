@@ -1,0 +1,86 @@
+"""End-to-end cSGHMC step on ViT-L/32 (or ResNet-101): fused kernel vs the
+reference's per-tensor torch-op update (methods/csghmc.py:747-778 as written,
+running on the same GPU).  Informational; not the bench metric."""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bayesdll_amd.csghmc as csghmc  # noqa: E402
+from bayesdll_amd.backbones import backbone  # noqa: E402
+
+
+def reference_update(net, moms, lrs, prior_sig, alpha, N, nd, should_sample):
+    """methods/csghmc.py:747-778, per tensor, torch ops (the reference on a GPU)."""
+    with torch.no_grad():
+        for (pname, p) in net.named_parameters():
+            lr = lrs[1] if net.readout_name in pname else lrs[0]
+            v = moms[pname]
+            grad_u = p.grad + prior_sig * p.data
+            noise = nd * np.sqrt((2 * alpha * lr)) / N * torch.randn_like(p)
+            v = v * (1 - alpha) - lr * grad_u + (noise if should_sample else 0)
+            moms[pname] = v
+            p.data.add_(v)
+
+
+def main():
+    name = os.environ.get("BACKBONE", "vit_l_32")
+    batch = int(os.environ.get("BATCH", "16"))
+    steps = int(os.environ.get("STEPS", "10"))
+    dev = "cuda"
+    x = torch.randn(batch, 3, 224, 224, device=dev)
+    y = torch.randint(0, 1000, (batch,), device=dev)
+    crit = torch.nn.CrossEntropyLoss()
+    lrs = [1e-4, 1e-2]
+    res = {}
+    for mode in ("reference_torch_ops", "fused"):
+        torch.manual_seed(0)
+        net = backbone(name, 1000).to(dev)
+        model = csghmc.Model(ND=1840, prior_sig=1.0, momentum_decay=0.18)
+        moms = {n: torch.zeros_like(p) for n, p in net.named_parameters()}
+        fwdbwd = upd = 0.0
+        for k in range(steps + 3):
+            if k == 3:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            ss = k % 10 == 0
+            if mode == "fused":
+                model(x, y, net, None, crit, lrs, 1.0, 0.01, should_sample=ss)
+            else:
+                out = net(x)
+                loss = crit(out, y)
+                net.zero_grad()
+                loss.backward()
+                reference_update(net, moms, lrs, 1.0, 0.18, 1840.0, 0.01, ss)
+                loss.item()
+        torch.cuda.synchronize()
+        res[mode] = (time.perf_counter() - t0) / steps * 1e3
+        # update-only timing
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if mode == "fused":
+            from bayesdll_amd import _lib as L
+            from bayesdll_amd import kernels as K
+            st = model.flat
+            e0.record()
+            for _ in range(steps):
+                K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=(1e-7, 1e-6),
+                              noise_mode=L.NOISE_PHILOX, one_minus_alpha=0.82, prior_sig=1.0)
+            e1.record()
+        else:
+            e0.record()
+            for _ in range(steps):
+                reference_update(net, moms, lrs, 1.0, 0.18, 1840.0, 0.01, True)
+            e1.record()
+        torch.cuda.synchronize()
+        res[mode + "_update_only"] = e0.elapsed_time(e1) / steps
+        del net, model, moms
+        torch.cuda.empty_cache()
+    for k, v in res.items():
+        print(f"{name} batch {batch}: {k}: {v:.3f} ms/step")
+
+
+if __name__ == "__main__":
+    main()

@@ -7,7 +7,7 @@
   16-B/lane streaming read, so bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024;
 * profiles/pmc_traffic.json updated (read by bench.py for roofline.traffic).
 
-usage: python tools/pmc_summary.py <tag>
+usage: python tools/pmc_summary.py <tag> [dest subdir, e.g. round1/kernel_v3]
 """
 import csv
 import json
@@ -27,9 +27,9 @@ def kind_of(name):
     return KIND.get((int(m.group(2)), int(m.group(3))))
 
 
-def main(tag):
+def main(tag, dest=None):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
-    dst = os.path.join(ROOT, "profiles", tag)
+    dst = os.path.join(ROOT, "profiles", dest or tag)
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(dst, "bench_kernel_stats.csv"))
@@ -53,7 +53,7 @@ def main(tag):
         raw[k] = {c: sum(v) / len(v) for c, v in d.items()}
         if "FETCH_SIZE" in raw[k] and "WRITE_SIZE" in raw[k]:
             traffic[k] = int((2 * raw[k]["FETCH_SIZE"] + raw[k]["WRITE_SIZE"]) * 1024)
-    out = {"vit_l_32": traffic, "_source": f"profiles/{tag}",
+    out = {"vit_l_32": traffic, "_source": f"profiles/{dest or tag}",
            "_method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; bytes "
                       "per launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE "
                       "reports half of a 16-B/lane streaming read, MI355X_MICROARCH.md)",
@@ -63,4 +63,4 @@ def main(tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
