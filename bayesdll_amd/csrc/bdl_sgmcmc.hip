@@ -45,7 +45,7 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes
 
 // Tunables (bdl_set_launch_config).  blocks_per_cu * 256 CUs workgroups, each
 // lane keeps kUnroll float4 groups in flight per iteration.
-// Defaults from the gfx950 sweep (tools/sweep.py, profiles/r01/sweep_*.log):
+// Defaults from the gfx950 sweep (tools/sweep.py, profiles/round1/kernel_v1/sweep_*.log):
 // grid-stride with 2 workgroups/CU and 1 float4 group in flight per lane,
 // non-temporal 16-B loads and stores, measured best on every kernel kind.
 int g_blocks_per_cu = 2;

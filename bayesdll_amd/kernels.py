@@ -105,7 +105,7 @@ def set_launch_config(blocks_per_cu=0, unroll=0, grid_stride=0):
 
 
 # Launch geometries worth trying on gfx950 (workgroups/CU, float4 groups in
-# flight per lane, grid-stride): the sweep (profiles/r01) shows the optimum
+# flight per lane, grid-stride): the sweep (profiles/round1/kernel_v1) shows the optimum
 # moving between these from one device to the next.
 AUTOTUNE_CANDIDATES = ((2, 1, 1), (1, 4, 1), (3, 1, 1), (2, 4, 1), (1, 2, 1))
 
