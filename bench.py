@@ -33,7 +33,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-BYTES_PER_ELEM = {"explore": 20, "sample": 20, "collect_init": 28, "collect": 36}
+BYTES_PER_ELEM = {"explore": 20, "sample": 20, "collect_init": 28, "collect": 36,
+                  # sgld + SGD(momentum): theta rw, g r, theta0 r, buf (w | rw), +m1/m2 rw
+                  "sgld_first": 20, "sgld": 24, "sgld_collect": 40}
 
 
 def parse():
@@ -42,6 +44,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--backbone", default="vit_l_32")
+    ap.add_argument("--method", default="csghmc", choices=["csghmc", "sgld"])
     ap.add_argument("--num-classes", type=int, default=1000)
     ap.add_argument("--thin", type=int, default=10)
     ap.add_argument("--cycles", type=int, default=4)
@@ -62,8 +65,15 @@ def dist_setup():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("BDL_BENCH_BACKEND", "nccl")  # nccl == RCCL on ROCm
+        if backend == "gloo":
+            # rehearsal of the N-rank path on fewer GPUs (ranks may share a device)
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         return dist, rank, world, local
     torch.cuda.set_device(local)
     return None, 0, 1, local
@@ -159,18 +169,53 @@ def main():
     else:
         launch = {"default": True, "autotuned": False}
     dev = torch.device("cuda", local)
-    st = FlatState.from_segments(segs, readout, device=dev)
+    sgld = a.method == "sgld"
+    st = FlatState.from_segments(segs, readout, device=dev, need_prior=sgld)
     gen = torch.Generator(device=dev).manual_seed(42 + rank)
-    st.theta.normal_(0.0, 0.02, generator=gen)
+    if sgld:  # config 3: theta0 ~ N(0, 0.02^2) (pretrained stand-in), theta = theta0 + N(0, 1e-3^2)
+        st.prior.normal_(0.0, 0.02, generator=gen)
+        st.theta.normal_(0.0, 1e-3, generator=gen).add_(st.prior)
+    else:
+        st.theta.normal_(0.0, 0.02, generator=gen)
     st.grad.normal_(0.0, 1e-3, generator=gen)
     n = st.n
 
-    # config 4 hyper-parameters
+    # config 4 hyper-parameters; config 3 for --method sgld
     lr, lr_head, alpha, nd, ND, Ninflate, prior_sig = 1e-4, 1e-2, 0.18, 0.01, 1840, 1.0, 1.0
+    if sgld:
+        Ninflate, mu = 1e3, 0.5
     N = ND * Ninflate
     total = a.warmup + a.steps
     sched = CyclicalSGMCMC(lr, a.cycles, 1, 0.5)  # one "epoch" of `total` batches
     m1s, m2s, spc = {}, {}, {}
+    if sgld:  # sgld.py:95-102 burn-in seeding (burnin = 0), outside the timed region
+        m1s[0] = torch.empty(n, dtype=torch.float32, device=dev)
+        m2s[0] = torch.empty(n, dtype=torch.float32, device=dev)
+        K.moments_update(st.theta, m1s[0], m2s[0], L.COLLECT_MEAN_INIT)
+        spc[0] = 1
+
+    def sgld_step(k, ev=None):
+        """methods/sgld.py:193-250: Model + SGD(momentum 0.5) + running moments
+        every `thin` iterations, fused."""
+        first = k == 0
+        collect = (k + 1) % a.thin == 0
+        kind = "sgld_first" if first else ("sgld_collect" if collect else "sgld")
+        lrs = (lr, lr_head)
+        ns = [nd * np.sqrt(2 / (N * x)) for x in lrs]
+        cnt = spc[0]
+        if ev is not None:
+            ev[0].record()
+        K.sgmcmc_step(st, L.SGLD, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_PHILOX,
+                      prior_sig=prior_sig, sigma2=prior_sig ** 2, n_data=N, mu=mu,
+                      first_step=first, momentum=True,
+                      collect=L.COLLECT_MEAN if collect else L.COLLECT_NONE, mom1=m1s[0],
+                      mom2=m2s[0], collect_a=float(cnt), collect_b=float(cnt + 1),
+                      seed=42 + rank, chain=rank, step=k)
+        if ev is not None:
+            ev[1].record()
+        if collect:
+            spc[0] = cnt + 1
+        return kind
 
     def plan(k):
         cur = sched.calculate_lr(0, k, total)
@@ -209,6 +254,8 @@ def main():
             spc[c] = cnt + 1
         return kind
 
+    if sgld:
+        step = sgld_step  # noqa: F811
     for k in range(a.warmup):
         step(k)
     torch.cuda.synchronize()
@@ -225,8 +272,9 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist is not None:  # max over ranks (outside the timed region)
+        on_dev = dist.get_backend() != "gloo"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if on_dev else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     assert torch.isfinite(st.theta[:1 << 20]).all()
@@ -269,7 +317,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (random-init theta, resident synthetic grad buffer)",
-        "config": {"workload": f"{a.backbone} cSGHMC fused leapfrog update (config 4/5)",
+        "config": {"workload": (f"{a.backbone} cSGHMC fused leapfrog update (config 4/5)" if not sgld
+                                else f"{a.backbone} SGLD + SGD(momentum 0.5) fused update (config 3)"),
                    "params": n, "tensors": len(segs), "readout": readout,
                    "cycles": a.cycles, "thin": a.thin, "beta": 0.5, "noise": "philox",
                    "parallelism": f"{world} independent chains (1/GPU)"},
@@ -281,13 +330,13 @@ def main():
                      "traffic": traffic,
                      "alg_bytes_per_launch": alg_bytes},
     }
-    if world == 1 and a.e2e_steps > 0 and a.backbone == "vit_l_32":
+    if world == 1 and a.e2e_steps > 0 and a.backbone == "vit_l_32" and not sgld:
         del st, m1s, m2s
         torch.cuda.empty_cache()
         e2e = e2e_steps(a.e2e_steps, 3, local, 42)
         e2e["fused_update_share"] = round(dom["avg_ms"] / e2e["ms_per_step"], 4)
         out["e2e"] = e2e
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not sgld:
         out["cpu_baseline"] = cpu_baseline(segs, readout, a.cpu_baseline_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
