@@ -25,7 +25,7 @@ def make_args(fx, tmp, device, **over):
     return SimpleNamespace(**a)
 
 
-def replay(fx, device="cuda", noise_mode="external", div_mode=None, runner_hook=None):
+def replay(fx, device="cuda", noise_mode="external", div_mode="true", runner_hook=None):
     import bayesdll_amd.csghmc as csghmc
     import bayesdll_amd.csgld as csgld
     import bayesdll_amd.sghmc as sghmc

@@ -161,7 +161,7 @@ def test_edge_sizes_csghmc_and_sgld(n):
     st2 = _state(segs, "fc", bias="uninformative", need_noise=True, need_prior=True, seed=5)
     th_ref, b_ref = ref_sgld(st2, lrs, ns, 0.8, 50.0, 0.9, False, recip=False)
     K.sgmcmc_step(st2, L.SGLD, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_BUFFER, sigma2=0.8 ** 2,
-                  n_data=50.0, mu=0.9, momentum=True, first_step=False)
+                  n_data=50.0, mu=0.9, momentum=True, first_step=False, div_mode="true")
     torch.cuda.synchronize()
     assert torch.equal(st2.mom, b_ref)
     np.testing.assert_allclose(st2.theta.cpu().numpy(), th_ref.cpu().numpy(), rtol=2e-7, atol=0)
