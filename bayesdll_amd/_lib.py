@@ -73,6 +73,8 @@ EXPORTS = {
                                  C.c_int32]),
     "bdl_sgmcmc_step": (C.c_int, [C.POINTER(StepArgs), C.c_void_p]),
     "bdl_moments_update": (C.c_int, [C.POINTER(MomentsArgs), C.c_void_p]),
+    "bdl_clip_workspace_bytes": (C.c_int64, [C.c_int64]),
+    "bdl_sgld_step_clipped": (C.c_int, [C.POINTER(StepArgs), C.c_float, C.c_void_p, C.c_void_p]),
     "bdl_posterior_sample": (C.c_int, [C.POINTER(SampleArgs), C.c_void_p]),
     "bdl_philox_normal": (C.c_int, [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint64,
                                     C.c_void_p]),

@@ -101,6 +101,19 @@ def save_logits(args, targets, logits, logits_all, suffix=None):
     return fname
 
 
+def load_checkpoint(path, device):
+    """torch.load with weights_only=True plus the numpy types the reference's
+    checkpoints contain (cycle_likelihoods are np.ndarray, methods/csghmc.py:377):
+    nothing from the file is executed."""
+    import numpy as _np
+    from torch.serialization import safe_globals
+    allowed = [_np.ndarray, _np.dtype, _np._core.multiarray._reconstruct]
+    allowed += [getattr(_np.dtypes, n) for n in ("Float64DType", "Float32DType", "Int64DType")
+                if hasattr(_np.dtypes, n)]
+    with safe_globals(allowed):
+        return torch.load(path, map_location=device, weights_only=True)
+
+
 def gmm_weights(cycle_likelihoods):
     """methods/csghmc.py:641-670: w_c = 1 / mean(1/lik), normalised."""
     if not cycle_likelihoods:

@@ -241,7 +241,7 @@ class Runner:
 
     def load_ckpt(self, ckpt_path):
         """methods/csghmc.py:552-566 (same keys restored)."""
-        ckpt = torch.load(ckpt_path, map_location=self.args.device, weights_only=True)
+        ckpt = R.load_checkpoint(ckpt_path, self.args.device)
         self.cycle_theta_mom1 = ckpt.get("cycle_theta_mom1", {})
         self.cycle_theta_mom2 = ckpt.get("cycle_theta_mom2", {})
         self.cycle_likelihoods = ckpt.get("cycle_likelihoods", {})

@@ -176,6 +176,7 @@ struct KArgs {
   float lr0, lr1, ns0, ns1;
   float one_minus_alpha, prior_sig, sigma2, n_data, mu, ca, cb;
   uint64_t seed, chain, step;
+  const float* __restrict__ clip;  // (total_norm, coef) from the clip finalize, or null
 };
 
 // Scalar division in the reference's rounding: torch CPU divides (x / s);
@@ -215,8 +216,8 @@ __device__ __forceinline__ int find_run_lds(int nruns, int64_t idx) {
 }
 
 struct StepConst {
-  bool sgd_mom, sgd_mom_read, has_m2, grad_ready;
-  float inv_s2, inv_nd, inv_ca, inv_cb;
+  bool sgd_mom, sgd_mom_read, has_m2, grad_ready, clip;
+  float inv_s2, inv_nd, inv_ca, inv_cb, clip_coef;
 };
 
 // ---------------------------------------------------------------------------
@@ -275,6 +276,7 @@ __device__ __forceinline__ void update_core(const KArgs& a, const StepConst& c, 
       gp = g + nz;
     }
     if constexpr (METHOD == BDL_SGLD) {
+      if (c.clip) gp = gp * c.clip_coef;  // clip_grad_norm_: grads.mul_(clip_coef_clamped)
       float stepv = gp;
       if (c.sgd_mom) {  // torch SGD momentum buffer
         v = (a.flags & BDL_FLAG_FIRST_STEP) ? gp : (a.mu * v + gp);
@@ -475,6 +477,8 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
   c.sgd_mom_read = c.sgd_mom && !(a.flags & BDL_FLAG_FIRST_STEP);
   c.has_m2 = (COLLECT != BDL_COLLECT_NONE) && (a.mom2 != nullptr);
   c.grad_ready = (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) && (a.flags & BDL_FLAG_GRAD_READY);
+  c.clip = (METHOD == BDL_SGLD) && a.clip != nullptr;
+  c.clip_coef = c.clip ? a.clip[1] : 1.0f;
   c.inv_s2 = 1.0f / a.sigma2;
   c.inv_nd = 1.0f / a.n_data;
   c.inv_ca = 1.0f / a.ca;
@@ -522,6 +526,145 @@ __global__ __launch_bounds__(kBlock) void bdl_step_kernel(const KArgs a) {
     step_body<METHOD, NOISE, COLLECT, true, UNROLL>(a);
   else
     step_body<METHOD, NOISE, COLLECT, false, UNROLL>(a);
+}
+
+// ---------------------------------------------------------------------------
+// Gradient-norm reduction for clip_grad_norm_ (csgld.py:250-251).  The SGLD
+// sampler gradient G = g + prior + noise is recomputed per element (Philox
+// noise is a pure function of its counter, so G is never stored) and
+// sum(G^2) reduced: per-lane fp32 fmaf accumulation, a 64-lane wavefront
+// butterfly (__shfl_xor), the block's 4 wave sums through LDS, one partial per
+// workgroup.  A single-workgroup finalize sums the partials in a fixed order
+// (fp64, deterministic) and writes (total_norm, coef).
+// ---------------------------------------------------------------------------
+constexpr int kMaxNormPartials = 2048;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int NOISE, bool RECIP, bool PRIOR>
+__device__ __forceinline__ float sqnorm_fast(const KArgs& a, const StepConst& c, int64_t gb,
+                                             float ns, float acc) {
+  constexpr int U = 2;
+  f4v th[U], g[U], t0[U], ep[U];
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+    t0[u] = ep[u] = z;
+    th[u] = vload(a.theta + e);
+    g[u] = vload(a.grad + e);
+    if constexpr (PRIOR) t0[u] = vload(a.prior_mean + e);
+    if constexpr (NOISE == BDL_NOISE_BUFFER) ep[u] = vload(a.noise + e);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float xt = th[u][j], xg = g[u][j], xv = 0.f;
+      update_core<BDL_SGLD_GRAD, NOISE, RECIP, PRIOR, false>(a, c, 0.f, ns, xt, xg, xv, t0[u][j],
+                                                             ep[u][j]);
+      acc = fmaf(xg, xg, acc);
+    }
+  }
+  return acc;
+}
+
+template <int NOISE, bool RECIP>
+__device__ __forceinline__ void sqnorm_body(const KArgs& a, float* __restrict__ partials) {
+  __shared__ float s_wave[kBlock / 64];
+  constexpr int64_t kIter = (int64_t)kBlock * 2;
+  StepConst c;
+  c.sgd_mom = c.sgd_mom_read = c.has_m2 = c.grad_ready = c.clip = false;
+  c.inv_s2 = 1.0f / a.sigma2;
+  c.inv_nd = 1.0f / a.n_data;
+  c.inv_ca = c.inv_cb = c.clip_coef = 1.0f;
+  const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
+  for (int i = threadIdx.x; i < a.nruns; i += kBlock) s_runs[i] = a.runs[i];
+  __syncthreads();
+  float acc = 0.f;
+  int r = find_run_lds(a.nruns, (int64_t)blockIdx.x * kIter * 4);
+  for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {
+    while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
+    const int64_t gend = min(gb + kIter, ngroups);
+    const uint32_t attr = run_attr(r);
+    if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 && !(attr & BDL_ATTR_SKIP)) {
+      const float ns = (attr & BDL_ATTR_HEAD) ? a.ns1 : a.ns0;
+      if (attr & BDL_ATTR_PRIOR)
+        acc = sqnorm_fast<NOISE, RECIP, true>(a, c, gb, ns, acc);
+      else
+        acc = sqnorm_fast<NOISE, RECIP, false>(a, c, gb, ns, acc);
+    } else {
+      for (int u = 0; u < 2; ++u) {
+        const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+        if (gi >= gend) continue;
+        const int64_t e = gi * 4;
+        const f4v z = {0.f, 0.f, 0.f, 0.f};
+        const f4v th = ld4(a.theta, e, a.n), g = ld4(a.grad, e, a.n);
+        const f4v t0 = ld4(a.prior_mean, e, a.n);
+        f4v ep = z;
+        if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, a.n);
+        if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+        for (int j = 0; j < 4; ++j) {
+          if (e + j >= a.n) break;
+          const uint32_t at = run_attr(find_run_lds(a.nruns, e + j));
+          if (at & BDL_ATTR_SKIP) continue;  // .grad is None: not in the norm
+          float xt = th[j], xg = g[j], xv = 0.f;
+          const float ns = (at & BDL_ATTR_HEAD) ? a.ns1 : a.ns0;
+          if (at & BDL_ATTR_PRIOR)
+            update_core<BDL_SGLD_GRAD, NOISE, RECIP, true, false>(a, c, 0.f, ns, xt, xg, xv, t0[j], ep[j]);
+          else
+            update_core<BDL_SGLD_GRAD, NOISE, RECIP, false, false>(a, c, 0.f, ns, xt, xg, xv, t0[j], ep[j]);
+          acc = fmaf(xg, xg, acc);
+        }
+      }
+    }
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) t += s_wave[w];
+    partials[blockIdx.x] = t;
+  }
+}
+
+template <int NOISE>
+__global__ __launch_bounds__(kBlock) void bdl_sqnorm_kernel(const KArgs a, float* partials) {
+  if (a.flags & BDL_FLAG_RECIP_DIV)
+    sqnorm_body<NOISE, true>(a, partials);
+  else
+    sqnorm_body<NOISE, false>(a, partials);
+}
+
+__global__ __launch_bounds__(kBlock) void bdl_clip_finalize_kernel(const float* __restrict__ partials,
+                                                                   int nparts, float max_norm,
+                                                                   float* __restrict__ out) {
+  __shared__ double s_d[kBlock / 64];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += kBlock) acc += (double)partials[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if ((threadIdx.x & 63) == 0) s_d[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < kBlock / 64; ++w) t += s_d[w];
+    const float norm = (float)sqrt(t);
+    // clip_grad_norm_: clip_coef = max_norm / (total_norm + 1e-6) (Tensor.__rtruediv__
+    // = reciprocal() * other), clamped at 1.0
+    float coef = (1.0f / (norm + 1e-6f)) * max_norm;
+    coef = fminf(coef, 1.0f);
+    out[0] = norm;
+    out[1] = coef;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -715,60 +858,9 @@ int grid_for(int64_t ngroups, int per_block_groups) {
   return (int)std::max<int64_t>(1, std::min(want, cap));
 }
 
-}  // namespace
-
-extern "C" {
-
-int bdl_version(void) { return BDL_ABI_VERSION; }
-
-const char* bdl_last_error(void) { return g_last_error.c_str(); }
-
-int bdl_set_launch_config(int32_t blocks_per_cu, int32_t unroll, int32_t grid_stride) {
-  const int prev = (g_grid_stride << 24) | (g_blocks_per_cu << 8) | g_unroll;
-  g_blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : 2;
-  g_unroll = (unroll == 1 || unroll == 2 || unroll == 4) ? unroll : 1;
-  g_grid_stride = grid_stride > 0 ? 1 : 0;
-  return prev;
-}
-
-int bdl_build_runs(const bdl_segment* segs, int32_t nseg, int64_t n, bdl_run* out, int32_t max_runs) {
-  if (!out || (nseg > 0 && !segs)) return fail(BDL_ERR_NULL, "bdl_build_runs: null pointer");
-  if (n < 0 || nseg < 0 || max_runs < 1) return fail(BDL_ERR_ARG, "bdl_build_runs: bad sizes");
-  int nr = 0;
-  int64_t pos = 0;
-  auto push = [&](int64_t end, uint32_t attr) -> bool {
-    if (end <= pos) return true;
-    if (nr > 0 && out[nr - 1].attr == attr) {
-      out[nr - 1].end = end;
-    } else {
-      if (nr >= max_runs) return false;
-      out[nr].end = end;
-      out[nr].attr = attr;
-      out[nr].pad = 0;
-      ++nr;
-    }
-    pos = end;
-    return true;
-  };
-  for (int i = 0; i < nseg; ++i) {
-    const bdl_segment& s = segs[i];
-    if (s.offset < pos || s.numel < 0 || s.offset + s.numel > n)
-      return fail(BDL_ERR_RUNS, "bdl_build_runs: segments overlap, are unsorted or exceed n");
-    if (!push(s.offset, BDL_ATTR_SKIP)) return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
-    if (!push(s.offset + s.numel, s.attr & 7u))
-      return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
-  }
-  if (!push(n, BDL_ATTR_SKIP)) return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
-  if (nr == 0) {  // n == 0: one empty run keeps the table well-formed
-    out[0].end = 0;
-    out[0].attr = BDL_ATTR_SKIP;
-    out[0].pad = 0;
-    nr = 1;
-  }
-  return nr;
-}
-
-int bdl_sgmcmc_step(const bdl_step_args* s, void* stream) {
+// Validate a step descriptor, pick the kernel instance and launch it; `clip`
+// (device pointer to (norm, coef)) scales the SGLD sampler gradient when set.
+int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   if (!s) return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: null args");
   if (s->n < 0) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: n < 0");
   if (s->method < BDL_CSGHMC || s->method > BDL_SGLD_GRAD)
@@ -839,15 +931,142 @@ int bdl_sgmcmc_step(const bdl_step_args* s, void* stream) {
   a.seed = s->seed;
   a.chain = s->chain;
   a.step = s->step;
+  a.clip = clip;
 
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kBlock), (size_t)s->nruns * sizeof(bdl_run),
-                     (hipStream_t)stream, a);
+                     stream, a);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     g_last_error = std::string("bdl_sgmcmc_step: launch failed: ") + hipGetErrorString(err);
     return BDL_ERR_LAUNCH;
   }
   return BDL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bdl_version(void) { return BDL_ABI_VERSION; }
+
+const char* bdl_last_error(void) { return g_last_error.c_str(); }
+
+int bdl_set_launch_config(int32_t blocks_per_cu, int32_t unroll, int32_t grid_stride) {
+  const int prev = (g_grid_stride << 24) | (g_blocks_per_cu << 8) | g_unroll;
+  g_blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : 2;
+  g_unroll = (unroll == 1 || unroll == 2 || unroll == 4) ? unroll : 1;
+  g_grid_stride = grid_stride > 0 ? 1 : 0;
+  return prev;
+}
+
+int bdl_build_runs(const bdl_segment* segs, int32_t nseg, int64_t n, bdl_run* out, int32_t max_runs) {
+  if (!out || (nseg > 0 && !segs)) return fail(BDL_ERR_NULL, "bdl_build_runs: null pointer");
+  if (n < 0 || nseg < 0 || max_runs < 1) return fail(BDL_ERR_ARG, "bdl_build_runs: bad sizes");
+  int nr = 0;
+  int64_t pos = 0;
+  auto push = [&](int64_t end, uint32_t attr) -> bool {
+    if (end <= pos) return true;
+    if (nr > 0 && out[nr - 1].attr == attr) {
+      out[nr - 1].end = end;
+    } else {
+      if (nr >= max_runs) return false;
+      out[nr].end = end;
+      out[nr].attr = attr;
+      out[nr].pad = 0;
+      ++nr;
+    }
+    pos = end;
+    return true;
+  };
+  for (int i = 0; i < nseg; ++i) {
+    const bdl_segment& s = segs[i];
+    if (s.offset < pos || s.numel < 0 || s.offset + s.numel > n)
+      return fail(BDL_ERR_RUNS, "bdl_build_runs: segments overlap, are unsorted or exceed n");
+    if (!push(s.offset, BDL_ATTR_SKIP)) return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
+    if (!push(s.offset + s.numel, s.attr & 7u))
+      return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
+  }
+  if (!push(n, BDL_ATTR_SKIP)) return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
+  if (nr == 0) {  // n == 0: one empty run keeps the table well-formed
+    out[0].end = 0;
+    out[0].attr = BDL_ATTR_SKIP;
+    out[0].pad = 0;
+    nr = 1;
+  }
+  return nr;
+}
+
+int bdl_sgmcmc_step(const bdl_step_args* s, void* stream) {
+  return launch_step(s, nullptr, (hipStream_t)stream);
+}
+
+int64_t bdl_clip_workspace_bytes(int64_t n) {
+  (void)n;
+  return (int64_t)(4 + kMaxNormPartials) * (int64_t)sizeof(float);
+}
+
+int bdl_sgld_step_clipped(const bdl_step_args* s, float max_norm, void* workspace, void* stream) {
+  if (!s) return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: null args");
+  if (!workspace) return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: null workspace");
+  if (!aligned16(workspace)) return fail(BDL_ERR_ALIGN, "bdl_sgld_step_clipped: workspace not 16-B aligned");
+  if (s->method != BDL_SGLD)
+    return fail(BDL_ERR_ARG, "bdl_sgld_step_clipped: only the SGLD sampler clips its gradient");
+  if (s->flags & BDL_FLAG_GRAD_READY)
+    return fail(BDL_ERR_ARG, "bdl_sgld_step_clipped: GRAD_READY is incompatible with clipping");
+  if (!(max_norm > 0.0f)) return fail(BDL_ERR_ARG, "bdl_sgld_step_clipped: max_norm must be > 0");
+  if (s->n < 0) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: n < 0");
+  if (s->n == 0) return BDL_OK;
+  if (s->noise_mode < BDL_NOISE_NONE || s->noise_mode > BDL_NOISE_PHILOX)
+    return fail(BDL_ERR_ARG, "bdl_sgld_step_clipped: unknown noise mode");
+  if (!s->theta || !s->grad || !s->runs || !s->prior_mean || s->nruns < 1)
+    return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: theta, grad, prior_mean and runs are required");
+  if (s->nruns > kMaxRuns)
+    return fail(BDL_ERR_RUNS, "bdl_sgld_step_clipped: more than 4096 runs (merge parameter groups)");
+  if (s->noise_mode == BDL_NOISE_BUFFER && !s->noise)
+    return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: noise buffer is required");
+  hipStream_t st = (hipStream_t)stream;
+  float* ws = (float*)workspace;
+  float* partials = ws + 4;
+
+  KArgs a{};
+  a.theta = s->theta;
+  a.grad = s->grad;
+  a.prior_mean = s->prior_mean;
+  a.noise = s->noise;
+  a.runs = s->runs;
+  a.nruns = s->nruns;
+  a.flags = s->flags;
+  a.n = s->n;
+  a.ns0 = s->noise_scale[0];
+  a.ns1 = s->noise_scale[1];
+  a.sigma2 = s->sigma2;
+  a.n_data = s->n_data;
+  a.seed = s->seed;
+  a.chain = s->chain;
+  a.step = s->step;
+  const int64_t ngroups = (s->n + 3) / 4;
+  const int64_t iters = (ngroups + 2 * kBlock - 1) / (2 * kBlock);
+  const int64_t cap = std::min<int64_t>((int64_t)device_cu_count() * g_blocks_per_cu, kMaxNormPartials);
+  const int grid = (int)std::max<int64_t>(1, std::min(iters, cap));
+  const size_t shmem = (size_t)s->nruns * sizeof(bdl_run);
+  switch (s->noise_mode) {
+    case BDL_NOISE_NONE:
+      hipLaunchKernelGGL(bdl_sqnorm_kernel<BDL_NOISE_NONE>, dim3(grid), dim3(kBlock), shmem, st, a, partials);
+      break;
+    case BDL_NOISE_BUFFER:
+      hipLaunchKernelGGL(bdl_sqnorm_kernel<BDL_NOISE_BUFFER>, dim3(grid), dim3(kBlock), shmem, st, a, partials);
+      break;
+    default:
+      hipLaunchKernelGGL(bdl_sqnorm_kernel<BDL_NOISE_PHILOX>, dim3(grid), dim3(kBlock), shmem, st, a, partials);
+      break;
+  }
+  hipLaunchKernelGGL(bdl_clip_finalize_kernel, dim3(1), dim3(kBlock), 0, st, partials, grid, max_norm, ws);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    g_last_error = std::string("bdl_sgld_step_clipped: launch failed: ") + hipGetErrorString(err);
+    return BDL_ERR_LAUNCH;
+  }
+  return launch_step(s, ws, st);
 }
 
 int bdl_moments_update(const bdl_moments_args* m, void* stream) {

@@ -26,11 +26,10 @@ def _div_flag(div_mode=None):
     return L.FLAG_RECIP_DIV if (div_mode or DIV_MODE) == "recip" else 0
 
 
-def sgmcmc_step(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1.0,
-                prior_sig=0.0, sigma2=1.0, n_data=1.0, mu=0.0, first_step=False,
-                momentum=False, collect=L.COLLECT_NONE, mom1=None, mom2=None, collect_a=1.0,
-                collect_b=1.0, seed=0, chain=0, step=0, div_mode=None, noise=None, grad_ready=False):
-    """One fused update over `state` (a FlatState). Asynchronous."""
+def _step_args(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1.0,
+               prior_sig=0.0, sigma2=1.0, n_data=1.0, mu=0.0, first_step=False,
+               momentum=False, collect=L.COLLECT_NONE, mom1=None, mom2=None, collect_a=1.0,
+               collect_b=1.0, seed=0, chain=0, step=0, div_mode=None, noise=None, grad_ready=False):
     a = L.StepArgs()
     a.theta = state.theta.data_ptr()
     a.grad = state.grad.data_ptr()
@@ -60,7 +59,37 @@ def sgmcmc_step(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=
     a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     a.chain = int(chain) & 0xFFFFFFFFFFFFFFFF
     a.step = int(step) & 0xFFFFFFFFFFFFFFFF
+    return a
+
+
+def sgmcmc_step(state, method, **kw):
+    """One fused update over `state` (a FlatState). Asynchronous."""
+    a = _step_args(state, method, **kw)
     L.check(L.lib().bdl_sgmcmc_step(a, L.current_stream_handle(state.device)), "bdl_sgmcmc_step")
+
+
+def clip_workspace(state):
+    """Device scratch for sgld_step_clipped: (total_norm, coef) then per-workgroup
+    partial sums.  Cached on the FlatState."""
+    ws = getattr(state, "_clip_ws", None)
+    if ws is None:
+        nbytes = int(L.lib().bdl_clip_workspace_bytes(int(state.n)))
+        ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=state.device)
+        state._clip_ws = ws
+    return ws
+
+
+def sgld_step_clipped(state, max_norm, **kw):
+    """SGLD step with torch.nn.utils.clip_grad_norm_(max_norm) applied to the
+    sampler gradient first (methods/csgld.py:250-253), all on device: a norm
+    pass, a one-workgroup finalize and the update pass.  Returns the workspace
+    whose first two floats are (total_norm, clip_coef)."""
+    a = _step_args(state, L.SGLD, **kw)
+    ws = clip_workspace(state)
+    L.check(L.lib().bdl_sgld_step_clipped(a, float(max_norm), ws.data_ptr(),
+                                          L.current_stream_handle(state.device)),
+            "bdl_sgld_step_clipped")
+    return ws
 
 
 def moments_update(theta, mom1, mom2, collect, collect_a=1.0, collect_b=1.0, div_mode=None):

@@ -206,7 +206,7 @@ class Runner:
         """methods/sgld.py:388-398. The reference sets post_theta_cnt = epoch
         (:394); kept by default for drop-in parity, exact_count=True restores
         the saved count instead."""
-        ckpt = torch.load(ckpt_path, map_location=self.args.device, weights_only=True)
+        ckpt = R.load_checkpoint(ckpt_path, self.args.device)
         self.post_theta_mom1 = ckpt["post_theta_mom1"]
         if ckpt["post_theta_mom2"] is not None:
             self.post_theta_mom2 = ckpt["post_theta_mom2"]
@@ -255,15 +255,14 @@ class Model(FusedModelBase):
                 else collect
             mom = sgd.momentum != 0
             first = mom and not sgd.has_buffer
-            grad_ready = False
+            kw = dict(common, lrs=sgd.lrs(), mu=sgd.momentum, first_step=first, momentum=mom,
+                      collect=ckind, mom1=m1, mom2=m2, collect_a=ca, collect_b=cb)
             if clip_grad is not None:
-                # csgld.py:250-251 clips between Model.forward and optimizer.step
-                K.sgmcmc_step(st, L.SGLD_GRAD, **common)
-                torch.nn.utils.clip_grad_norm_(net.parameters(), clip_grad)
-                grad_ready = True
-            K.sgmcmc_step(st, L.SGLD, **dict(common, lrs=sgd.lrs()), mu=sgd.momentum,
-                          first_step=first, momentum=mom, collect=ckind, mom1=m1, mom2=m2,
-                          collect_a=ca, collect_b=cb, grad_ready=grad_ready)
+                # csgld.py:250-253: clip_grad_norm_ between Model.forward and
+                # optimizer.step -- norm, coefficient and update all on device
+                K.sgld_step_clipped(st, clip_grad, **kw)
+            else:
+                K.sgmcmc_step(st, L.SGLD, **kw)
             if mom:
                 sgd.has_buffer = True
         self.step_count += 1

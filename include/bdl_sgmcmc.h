@@ -200,6 +200,24 @@ int bdl_sgmcmc_step(const bdl_step_args* args, void* hip_stream);
 /* Stand-alone moment update. */
 int bdl_moments_update(const bdl_moments_args* args, void* hip_stream);
 
+/* cSGLD with gradient clipping: replaces methods/csgld.py:248-253
+ * (Model.forward's p.grad = g + prior + noise, then
+ * torch.nn.utils.clip_grad_norm_(net.parameters(), clip_grad), then
+ * optimizer.step()).  args->method must be BDL_SGLD.  Three launches, no host
+ * synchronisation:
+ *   1. the sampler gradient G is recomputed element-wise (never stored: Philox
+ *      noise is a pure function of its counter) and sum(G^2) is reduced with
+ *      wavefront shuffles + LDS into one partial per workgroup (skipped
+ *      parameters excluded, as their .grad is None in the reference);
+ *   2. one workgroup sums the partials in a fixed order (deterministic),
+ *      total_norm = sqrt(sum), coef = min(1, max_norm / (total_norm + 1e-6));
+ *   3. the SGLD + SGD step on G * coef (moment collect allowed).
+ * workspace: device memory of bdl_clip_workspace_bytes(n) bytes; its first
+ * two floats receive (total_norm, coef) for inspection. */
+int64_t bdl_clip_workspace_bytes(int64_t n);
+int bdl_sgld_step_clipped(const bdl_step_args* args, float max_norm, void* workspace,
+                          void* hip_stream);
+
 /* theta_s = mean + sqrt(clamp(var)) * eps. */
 int bdl_posterior_sample(const bdl_sample_args* args, void* hip_stream);
 

@@ -144,6 +144,19 @@ def sgd_step(params, grads, bufs, lrs_per_param, momentum):
     return new_bufs
 
 
+def clip_grad_norm(grads, max_norm):
+    """torch.nn.utils.clip_grad_norm_(norm_type=2) as methods/csgld.py:250-251
+    calls it: per-tensor 2-norms, the 2-norm of those, coef = max_norm /
+    (total + 1e-6) clamped at 1, every gradient multiplied in place (also when
+    coef == 1).  Returns the total norm."""
+    norms = [torch.linalg.vector_norm(g, 2.0) for g in grads]
+    total = torch.linalg.vector_norm(torch.stack(norms), 2.0)
+    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    for g in grads:
+        g.mul_(coef)
+    return total
+
+
 def posterior_variance_raw(mom1, mom2, cnt):
     """methods/sgld.py:337-345: ratio*(m2 - m1^2) clamped at 1e-12."""
     ratio = cnt / (cnt - 1) if cnt > 1 else 1.0
@@ -239,6 +252,8 @@ def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
                                             for p, bb in zip(params, bufs)]))
                     newg = sgld_model(params, params0, g, names, readout, lrs, prior_sig, bias, N,
                                       nd, eps)
+                    if cfg.get("clip_grad") is not None:  # csgld.py:250-251
+                        clip_grad_norm(newg, cfg["clip_grad"])
                     bufs = sgd_step(params, newg, bufs, [lrs[1] if h else lrs[0] for h in is_head],
                                     cfg.get("momentum", 0.0))
                 step += 1
@@ -349,5 +364,6 @@ def csghmc_step_cpu(params, grads, moms, names, readout, lrs, prior_sig, momentu
 
 
 __all__ = ["CyclicalSchedule", "csghmc_update", "sghmc_model", "sgld_model", "sgd_step",
+           "clip_grad_norm",
            "posterior_variance_raw", "posterior_variance_welford", "posterior_sample", "simulate",
            "csghmc_step_cpu"]

@@ -108,7 +108,8 @@ def run_method(methods, method, cfg):
                      num_cycles=cfg.get("num_cycles", 2), lr=cfg["lr"], lr_head=cfg["lr_head"],
                      momentum=cfg.get("momentum", 0.0), ND=cfg["ND"],
                      proportion_exploration=cfg.get("beta", 0.5),
-                     hparams={k: str(v) for k, v in cfg["hparams"].items()})
+                     hparams={k: str(v) for k, v in cfg["hparams"].items()},
+                     **({"clip_grad": cfg["clip_grad"]} if "clip_grad" in cfg else {}))
     logger = logging.getLogger("golden")
     mod = getattr(methods, method)
     runner = mod.Runner(net, net0, args, logger)
@@ -196,6 +197,8 @@ def run_method(methods, method, cfg):
     return out
 
 
+CLIP_MAX_NORM = 40.0
+
 CONFIGS = {
     # cSGHMC (config 2 hyper-parameters, scaled to make every term visible)
     "csghmc_k20": ("csghmc", dict(epochs=4, bpe=5, num_cycles=2, beta=0.5, lr=0.05, lr_head=0.1,
@@ -216,6 +219,13 @@ CONFIGS = {
                                 grad_seed=103, grad_scale=0.5,
                                 hparams=dict(prior_sig=0.7, bias="informative", Ninflate=1.0,
                                              nd=1.0, nst=2, thin=2))),
+    # args.clip_grad: clip_grad_norm_ between Model.forward and optimizer.step
+    # (methods/csgld.py:250-251); max_norm chosen so some steps clip and some do not
+    "csgld_clip": ("csgld", dict(epochs=4, bpe=5, num_cycles=2, beta=0.5, lr=0.05, lr_head=0.1,
+                                 momentum=0.5, ND=50, torch_seed=19, init_seed=18, init_scale=0.5,
+                                 grad_seed=108, grad_scale=0.5, clip_grad=CLIP_MAX_NORM,
+                                 hparams=dict(prior_sig=0.7, bias="informative", Ninflate=1.0,
+                                              nd=1.0, nst=2, thin=2))),
     "sgld_inf": ("sgld", dict(epochs=3, bpe=5, lr=0.05, lr_head=0.1, momentum=0.5, ND=50,
                               torch_seed=10, init_seed=14, init_scale=0.5, grad_seed=104,
                               grad_scale=0.5, prior_seed=21,
@@ -379,10 +389,14 @@ def main():
             print(f"wrote {name}.npz draws={int(rec['draws'])} evals={int(rec['n_evals'])}")
         return
     for name, (method, cfg) in CONFIGS.items():
+        if only and name not in only.split(","):
+            continue
         rec = run_method(methods, method, copy.deepcopy(cfg))
         path = os.path.join(HERE, f"{name}.npz")
         np.savez_compressed(path, **rec)
         print(f"wrote {path}: steps={rec['lrs'].shape[0]} n={rec['theta'].shape[1]}")
+    if only:
+        return
     np.savez_compressed(os.path.join(HERE, "schedule.npz"), **schedule_tables(methods))
     print("wrote schedule.npz")
 

@@ -21,6 +21,8 @@ def make_args(fx, tmp, device, **over):
              proportion_exploration=cfg.get("beta", 0.5), full_sample=False, test_eval_freq=1,
              ece_num_bins=15, log_dir=tmp, num_classes=10,
              hparams={k: str(v) for k, v in cfg["hparams"].items()})
+    if cfg.get("clip_grad") is not None:
+        a["clip_grad"] = cfg["clip_grad"]
     a.update(over)
     return SimpleNamespace(**a)
 

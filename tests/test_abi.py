@@ -15,14 +15,14 @@ HEADER = os.path.join(ROOT, "include", "bdl_sgmcmc.h")
 
 def declared_functions():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(bdl_\w+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(bdl_\w+)\(", txt, re.M)))
 
 
 def test_header_declares_expected_api():
     assert declared_functions() == sorted([
         "bdl_version", "bdl_last_error", "bdl_build_runs", "bdl_sgmcmc_step",
         "bdl_moments_update", "bdl_posterior_sample", "bdl_philox_normal",
-        "bdl_set_launch_config"])
+        "bdl_set_launch_config", "bdl_clip_workspace_bytes", "bdl_sgld_step_clipped"])
 
 
 def test_library_loads_and_exports_every_declared_symbol():

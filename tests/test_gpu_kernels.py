@@ -283,3 +283,133 @@ def test_posterior_sample_matches_torch_formula():
     K.posterior_sample(out, m1, None, var_mode=L.VAR_GIVEN, noise=eps)
     torch.cuda.synchronize()
     assert torch.equal(out, m1 + torch.full_like(m1, 1e-12).sqrt() * eps)
+
+
+# ------------------------------------------------------- clipped SGLD (csgld)
+def ref_clip_sgld(st, max_norm, lrs, ns, sigma, N, mu, first):
+    """methods/csgld.py:250-253 on the device with torch ops: the sampler
+    gradient of csgld.py:665-680 per tensor, torch.nn.utils.clip_grad_norm_
+    over the tensors that have a gradient, then SGD(momentum)."""
+    th, buf = st.theta.clone(), st.mom.clone()
+    plist, segs = [], []
+    for (o, k, a) in zip(st.offsets, st.numels, st.attrs):
+        if a & 4:  # no .grad: not in the norm, not stepped
+            continue
+        h = 1 if a & 1 else 0
+        p, p0, g = th[o:o + k], st.prior[o:o + k], st.grad[o:o + k]
+        nz = ns[h] * st.noise[o:o + k]
+        gp = g + ((p - p0) / (sigma ** 2) / N + nz) if a & 2 else g + nz
+        w = torch.nn.Parameter(torch.empty(0, device=DEV))
+        w.grad = gp
+        plist.append(w)
+        segs.append((o, k, h))
+    total = torch.nn.utils.clip_grad_norm_(plist, max_norm)
+    for w, (o, k, h) in zip(plist, segs):
+        gp, b = w.grad, buf[o:o + k]
+        if mu != 0:
+            if first:
+                b.copy_(gp)
+            else:
+                b.mul_(mu).add_(gp)
+            gp = b
+        th[o:o + k].add_(gp, alpha=-lrs[h])
+    return th, buf, float(total)
+
+
+def _vec_rel(a, b):
+    return float((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-30))
+
+
+def _freeze(st, idx):
+    from bayesdll_amd.flat import build_runs, segment_attrs
+    st.requires_grad = [i not in idx for i in range(len(st.names))]
+    st.attrs = segment_attrs(st.names, st.readout_name, st.bias, st.requires_grad)
+    st.runs = build_runs(st.offsets, st.numels, st.attrs, st.n).to(st.device)
+    st.nruns = int(st.runs.shape[0])
+
+
+def _clipped_case(st, scale_vs_norm, first, mu=0.5, lrs=(1e-3, 2e-3), sigma=0.8, N=500.0, nd=0.05):
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd import _lib as L
+    ns = [nd * np.sqrt(2 / (N * lr)) for lr in lrs]
+    _, _, total = ref_clip_sgld(st, 1e30, lrs, ns, sigma, N, mu, first)
+    max_norm = scale_vs_norm * total
+    th_ref, b_ref, _ = ref_clip_sgld(st, max_norm, lrs, ns, sigma, N, mu, first)
+    th0, b0 = st.theta.clone(), st.mom.clone()
+    ws = K.sgld_step_clipped(st, max_norm, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_BUFFER,
+                             sigma2=sigma ** 2, n_data=N, mu=mu, first_step=first,
+                             momentum=mu != 0, div_mode="recip")
+    torch.cuda.synchronize()
+    norm, coef = ws[0].item(), ws[1].item()
+    assert abs(norm - total) <= 1e-5 * total
+    assert coef == pytest.approx(min(1.0, max_norm / (total + 1e-6)), rel=1e-5)
+    assert _vec_rel(st.theta, th_ref) <= 1e-5
+    assert _vec_rel(st.mom, b_ref) <= 1e-5
+    frozen = [(o, k) for o, k, a in zip(st.offsets, st.numels, st.attrs) if a & 4]
+    for o, k in frozen:  # untouched
+        assert torch.equal(st.theta[o:o + k], th0[o:o + k])
+        assert torch.equal(st.mom[o:o + k], b0[o:o + k])
+    st.theta.copy_(th0)
+    st.mom.copy_(b0)
+    return norm, coef
+
+
+@pytest.mark.parametrize("n", [1, 5, 17, 4097, 65537, 1 << 20])
+def test_clipped_sgld_edge_sizes_and_frozen_tensors(n):
+    rng = np.random.default_rng(n + 7)
+    cuts = sorted(set(rng.integers(1, n, size=min(7, max(n - 1, 0))).tolist())) if n > 1 else []
+    bounds = [0] + cuts + [n]
+    segs = []
+    for i in range(len(bounds) - 1):
+        name = ("fc." if i == len(bounds) - 2 else f"l{i}.") + ("bias" if i % 2 else "weight")
+        segs.append((name, (bounds[i + 1] - bounds[i],)))
+    st = _state(segs, "fc", bias="uninformative", need_noise=True, need_prior=True, seed=n)
+    if len(segs) > 2:
+        _freeze(st, {1})
+    for scale in (0.5, 2.0):
+        for first in (True, False):
+            _, coef = _clipped_case(st, scale, first)
+            assert (coef < 1.0) == (scale < 1.0)
+
+
+def test_clipped_sgld_full_size_vit():
+    """ViT-L/32 (306,535,400 params, 296 tensors): clipping active and inactive."""
+    from bayesdll_amd.shapes import vit_l_32
+    segs, readout = vit_l_32()
+    st = _state(segs, readout, need_prior=True, need_noise=True, seed=3)
+    _clipped_case(st, 0.25, False)
+    _clipped_case(st, 4.0, True, mu=0.0)
+
+
+def test_clipped_sgld_philox_equals_buffer():
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    segs = [("l0.weight", (300, 301)), ("l0.bias", (301,)), ("fc.weight", (10, 301)),
+            ("fc.bias", (10,))]
+    st = _state(segs, "fc", need_noise=True, need_prior=True, seed=11)
+    th0, b0 = st.theta.clone(), st.mom.clone()
+    kw = dict(lrs=(1e-3, 1e-2), noise_scale=(0.3, 0.1), sigma2=1.0, n_data=100.0, mu=0.9,
+              momentum=True, first_step=True, seed=1234, chain=2, step=9)
+    ws = K.sgld_step_clipped(st, 5.0, noise_mode=L.NOISE_PHILOX, **kw)
+    torch.cuda.synchronize()
+    th_p, b_p, ws_p = st.theta.clone(), st.mom.clone(), ws[:2].clone()
+    st.theta.copy_(th0)
+    st.mom.copy_(b0)
+    st.noise.copy_(K.philox_normal(st.n, 1234, 2, 9))
+    ws = K.sgld_step_clipped(st, 5.0, noise_mode=L.NOISE_BUFFER, **kw)
+    torch.cuda.synchronize()
+    assert ws_p[1].item() < 1.0
+    assert torch.equal(ws[:2], ws_p)
+    assert torch.equal(st.theta, th_p) and torch.equal(st.mom, b_p)
+
+
+def test_clipped_sgld_rejects_bad_arguments():
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    st = _state([("fc.weight", (64,))], "fc", need_noise=True, need_prior=True)
+    with pytest.raises(RuntimeError, match="max_norm"):
+        K.sgld_step_clipped(st, 0.0, lrs=(1e-3, 1e-3), noise_scale=(0.1, 0.1),
+                            noise_mode=L.NOISE_BUFFER)
+    with pytest.raises(RuntimeError, match="GRAD_READY"):
+        K.sgld_step_clipped(st, 1.0, lrs=(1e-3, 1e-3), noise_scale=(0.1, 0.1),
+                            noise_mode=L.NOISE_BUFFER, grad_ready=True)

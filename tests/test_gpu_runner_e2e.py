@@ -230,3 +230,40 @@ def test_mlp_real_autograd_matches_reference_update_same_gpu(method):
     got = model.flat.theta.cpu().numpy()
     assert rel(got, ref) <= 1e-5
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-7)
+
+
+def test_checkpoint_format_and_roundtrip(tmp_path):
+    """save_ckpt writes the reference's file names and keys
+    (methods/csghmc.py:530-549, methods/sgld.py:367-385) straight from the flat
+    buffers; load_ckpt restores them (weights_only loading)."""
+    import os
+    fx, runner, res, evals, prov = run_product("mlp_csghmc_c2")
+    files = sorted(os.listdir(runner.args.log_dir))
+    assert "1_ckpt.pt" in files and "2_ckpt.pt" in files and "logits_test.pkl" in files
+    from bayesdll_amd._runner import load_checkpoint
+    ck = load_checkpoint(os.path.join(runner.args.log_dir, "2_ckpt.pt"), "cpu")
+    assert set(ck) == {"last_theta", "cycle_theta_mom1", "cycle_theta_mom2", "cycle_likelihoods",
+                       "cycle_states", "epoch", "current_cycle", "samples_per_cycle"}
+    vec = torch.nn.utils.parameters_to_vector(runner.net.parameters()).detach().cpu()
+    assert torch.equal(ck["last_theta"], vec)
+    assert ck["samples_per_cycle"] == runner.samples_per_cycle and ck["current_cycle"] == 2
+    assert set(ck["cycle_states"][1]) == set(runner.net.state_dict())
+    epoch = runner.load_ckpt(os.path.join(runner.args.log_dir, "2_ckpt.pt"))
+    assert epoch == ck["epoch"]
+
+    fx, sg, res, evals, prov = run_product("mlp_sgld_c1")
+    ck = load_checkpoint(os.path.join(sg.args.log_dir, "ckpt.pt"), "cpu")
+    assert set(ck) == {"last_theta", "post_theta_mom1", "post_theta_mom2", "post_theta_cnt",
+                       "prior_sig", "optimizer", "epoch"}
+    # torch.optim.SGD layout: one momentum_buffer per parameter, = the flat buffer's views
+    bufs = [ck["optimizer"]["state"][i]["momentum_buffer"] for i in range(8)]
+    flatbuf = torch.cat([b.reshape(-1) for b in bufs])
+    st = sg.model.flat
+    # the checkpoint holds the buffer as of the save (best epoch); shape/layout check
+    assert flatbuf.numel() == st.n
+    assert set(ck["last_theta"]) == set(sg.net.state_dict())
+    cnt = sg.post_theta_cnt
+    sg.load_ckpt(os.path.join(sg.args.log_dir, "ckpt.pt"))
+    assert sg.post_theta_cnt == ck["epoch"]  # the reference's cnt = epoch (sgld.py:394)
+    sg.load_ckpt(os.path.join(sg.args.log_dir, "ckpt.pt"), exact_count=True)
+    assert sg.post_theta_cnt == ck["post_theta_cnt"] and ck["post_theta_cnt"] <= cnt
