@@ -294,12 +294,16 @@ def ref_clip_sgld(st, max_norm, lrs, ns, sigma, N, mu, first):
     plist, segs = [], []
     for (o, k, a) in zip(st.offsets, st.numels, st.attrs):
         if a & 4:  # no .grad: not in the norm, not stepped
+            if first and mu != 0:
+                # torch SGD holds no buffer for it; the flat buffer holds 0, so a
+                # later first gradient gives buf = mu*0 + g == clone(g)
+                buf[o:o + k].zero_()
             continue
         h = 1 if a & 1 else 0
         p, p0, g = th[o:o + k], st.prior[o:o + k], st.grad[o:o + k]
         nz = ns[h] * st.noise[o:o + k]
         gp = g + ((p - p0) / (sigma ** 2) / N + nz) if a & 2 else g + nz
-        w = torch.nn.Parameter(torch.empty(0, device=DEV))
+        w = torch.nn.Parameter(torch.empty_like(gp))
         w.grad = gp
         plist.append(w)
         segs.append((o, k, h))
@@ -346,9 +350,9 @@ def _clipped_case(st, scale_vs_norm, first, mu=0.5, lrs=(1e-3, 2e-3), sigma=0.8,
     assert _vec_rel(st.theta, th_ref) <= 1e-5
     assert _vec_rel(st.mom, b_ref) <= 1e-5
     frozen = [(o, k) for o, k, a in zip(st.offsets, st.numels, st.attrs) if a & 4]
-    for o, k in frozen:  # untouched
+    for o, k in frozen:  # theta untouched; buffer untouched after the first step
         assert torch.equal(st.theta[o:o + k], th0[o:o + k])
-        assert torch.equal(st.mom[o:o + k], b0[o:o + k])
+        assert torch.equal(st.mom[o:o + k], b_ref[o:o + k])
     st.theta.copy_(th0)
     st.mom.copy_(b0)
     return norm, coef
