@@ -5,6 +5,8 @@ Drop-in modules (same Runner/Model interfaces as the reference's methods/*.py):
     bayesdll_amd.sghmc    SGHMC           (methods/sghmc.py)
     bayesdll_amd.csgld    cyclical SGLD   (methods/csgld.py)
     bayesdll_amd.sgld     SGLD            (methods/sgld.py, src/bayesdll/sgld.py)
+    bayesdll_amd.adam_sghmc   Adam-preconditioned SGHMC          (methods/adam_sghmc.py)
+    bayesdll_amd.adam_csghmc  cyclical Adam-preconditioned SGHMC (methods/adam_csghmc.py)
     bayesdll_amd.cyclical CyclicalSGMCMC  (methods/cyclical.py)
 
 The per-step update runs in hand-written HIP kernels for gfx950

@@ -108,3 +108,15 @@ class FusedModelBase(nn.Module):
         if st is None or st.mom is None:
             return {}
         return dict(zip(st.names, st.views(st.mom)))
+
+    def load_momentum_buffer(self, d, flat=None):
+        """Copy a saved name -> tensor dict into the flat buffer (st.mom, or
+        `flat`), in place, so the kernel's pointers stay valid."""
+        st = self._state
+        if st is None:
+            raise RuntimeError("load the checkpoint after the first step has bound the state")
+        dst = st.mom if flat is None else flat
+        with torch.no_grad():
+            for nm, v in zip(st.names, st.views(dst)):
+                if nm in d:
+                    v.copy_(d[nm].reshape(v.shape))

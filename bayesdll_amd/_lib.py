@@ -18,13 +18,13 @@ LIB_PATH = os.environ.get("BDL_SGMCMC_LIB", os.path.join(HERE, "libbdl_sgmcmc.so
 
 # enums / bits — must match include/bdl_sgmcmc.h
 BDL_OK = 0
-CSGHMC, SGHMC, SGLD, SGHMC_GRAD, SGLD_GRAD = 0, 1, 2, 3, 4
+CSGHMC, SGHMC, SGLD, SGHMC_GRAD, SGLD_GRAD, ADAM_SGHMC, ADAM_SGHMC_GRAD = range(7)
 NOISE_NONE, NOISE_BUFFER, NOISE_PHILOX = 0, 1, 2
 COLLECT_NONE, COLLECT_WELFORD_INIT, COLLECT_WELFORD, COLLECT_MEAN_INIT, COLLECT_MEAN = range(5)
 ATTR_HEAD, ATTR_PRIOR, ATTR_SKIP = 0x1, 0x2, 0x4
 FLAG_FIRST_STEP, FLAG_RECIP_DIV, FLAG_MOMENTUM, FLAG_GRAD_READY = 0x1, 0x2, 0x4, 0x8
 VAR_GIVEN, VAR_RAW_MOMENTS, VAR_WELFORD = 0, 1, 2
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _fp = C.c_void_p
 
@@ -48,21 +48,34 @@ class StepArgs(C.Structure):
         ("lr", C.c_float * 2), ("noise_scale", C.c_float * 2),
         ("one_minus_alpha", C.c_float), ("prior_sig", C.c_float), ("sigma2", C.c_float),
         ("n_data", C.c_float), ("mu", C.c_float), ("collect_a", C.c_float),
-        ("collect_b", C.c_float), ("pad1", C.c_float),
+        ("collect_b", C.c_float), ("inv_sigma2", C.c_float), ("inv_n_data", C.c_float),
+        ("inv_collect_a", C.c_float), ("inv_collect_b", C.c_float), ("pad1", C.c_float),
         ("seed", C.c_uint64), ("chain", C.c_uint64), ("step", C.c_uint64),
     ]
+
+
+class AdamArgs(C.Structure):
+    _fields_ = [("adam_m", _fp), ("adam_v", _fp), ("sgd_buf", _fp),
+                ("beta1", C.c_float), ("one_minus_beta1", C.c_float), ("beta2", C.c_float),
+                ("one_minus_beta2", C.c_float), ("bias_corr1", C.c_float),
+                ("bias_corr2", C.c_float), ("eps", C.c_float), ("two_alpha", C.c_float),
+                ("nd", C.c_float), ("temperature", C.c_float), ("inv_bias_corr1", C.c_float),
+                ("inv_bias_corr2", C.c_float), ("inv_temperature", C.c_float),
+                ("pad2", C.c_float), ("grad_is_mom", C.c_int32), ("pad", C.c_int32)]
 
 
 class MomentsArgs(C.Structure):
     _fields_ = [("theta", _fp), ("mom1", _fp), ("mom2", _fp), ("n", C.c_int64),
                 ("collect", C.c_int32), ("flags", C.c_int32), ("collect_a", C.c_float),
-                ("collect_b", C.c_float)]
+                ("collect_b", C.c_float), ("inv_collect_a", C.c_float),
+                ("inv_collect_b", C.c_float)]
 
 
 class SampleArgs(C.Structure):
     _fields_ = [("out", _fp), ("mom1", _fp), ("mom2", _fp), ("noise", _fp), ("n", C.c_int64),
                 ("var_mode", C.c_int32), ("noise_mode", C.c_int32), ("ratio", C.c_float),
-                ("var_floor", C.c_float), ("seed", C.c_uint64), ("chain", C.c_uint64),
+                ("var_floor", C.c_float), ("inv_ratio", C.c_float), ("pad", C.c_float),
+                ("seed", C.c_uint64), ("chain", C.c_uint64),
                 ("step", C.c_uint64)]
 
 
@@ -73,6 +86,7 @@ EXPORTS = {
                                  C.c_int32]),
     "bdl_sgmcmc_step": (C.c_int, [C.POINTER(StepArgs), C.c_void_p]),
     "bdl_moments_update": (C.c_int, [C.POINTER(MomentsArgs), C.c_void_p]),
+    "bdl_adam_step": (C.c_int, [C.POINTER(StepArgs), C.POINTER(AdamArgs), C.c_void_p]),
     "bdl_clip_workspace_bytes": (C.c_int64, [C.c_int64]),
     "bdl_sgld_step_clipped": (C.c_int, [C.POINTER(StepArgs), C.c_float, C.c_void_p, C.c_void_p]),
     "bdl_posterior_sample": (C.c_int, [C.POINTER(SampleArgs), C.c_void_p]),

@@ -45,8 +45,7 @@ class Runner:
         self.net0 = self.net0.to(args.device)
         self.net = net.to(args.device)
         hparams = args.hparams
-        self.model = Model(ND=args.ND, prior_sig=float(hparams["prior_sig"]),
-                           bias=str(hparams["bias"])).to(args.device)
+        self.model = self._make_model(args, hparams).to(args.device)
         if getattr(args, "noise_mode", None):
             self.model.noise_mode = args.noise_mode
         if getattr(args, "seed", None) is not None:
@@ -56,8 +55,8 @@ class Runner:
                          if self.net.readout_name not in pn], "lr": args.lr},
              {"params": [p for pn, p in self.net.named_parameters()
                          if self.net.readout_name in pn], "lr": args.lr_head}],
-            momentum=args.momentum, weight_decay=0)
-        self.sgd = FusedSGD(self.optimizer, args.momentum)
+            momentum=self._momentum(args), weight_decay=0)
+        self.sgd = FusedSGD(self.optimizer, self._momentum(args))
         self.cyclical_scheduler = CyclicalSGMCMC(
             base_lr=args.lr,
             nbr_of_cycles=args.num_cycles if hasattr(args, "num_cycles") else 10,
@@ -78,8 +77,21 @@ class Runner:
         self.cycle_states = {}
         self.all_samples = {}
 
+    def _make_model(self, args, hparams):
+        return Model(ND=args.ND, prior_sig=float(hparams["prior_sig"]), bias=str(hparams["bias"]))
+
+    @staticmethod
+    def _momentum(args):
+        return args.momentum
+
     def _state(self):
         return self.model.state_for(self.net, self.net0)
+
+    def _cycle_end(self, cycle_number):
+        """Hook at every last_in_cycle step, before the cycle bookkeeping."""
+
+    def _cycle_completed(self, cycle_number):
+        """Hook after a newly completed cycle was scored and checkpointed."""
 
     def train(self, train_loader, val_loader, test_loader):
         args, logger = self.args, self.logger
@@ -171,6 +183,7 @@ class Runner:
             if last_in_cycle:
                 cycle_number = sched.get_cycle_number(epoch=ep, batch=batch_idx,
                                                       batches_per_epoch=bpe)
+                self._cycle_end(cycle_number)
                 self.cycle_states[cycle_number] = copy.deepcopy(self.net.state_dict())
                 if cycle_number > self.current_cycle:
                     cycle_updated = True
@@ -179,6 +192,7 @@ class Runner:
                     self.cycle_likelihoods[cycle_number] = likelihood
                     with torch.no_grad():
                         self.save_ckpt(epoch=sched.current_epoch)
+                    self._cycle_completed(cycle_number)
         return loss / nb, error / nb, cycle_updated
 
     def _variance_source(self, cycle):

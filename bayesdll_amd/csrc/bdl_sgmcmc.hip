@@ -177,7 +177,19 @@ struct KArgs {
   float one_minus_alpha, prior_sig, sigma2, n_data, mu, ca, cb;
   uint64_t seed, chain, step;
   const float* __restrict__ clip;  // (total_norm, coef) from the clip finalize, or null
+  // Adam-preconditioned SGHMC only (bdl_adam_step)
+  float* __restrict__ adam_m;
+  float* __restrict__ adam_v;
+  float* __restrict__ sgd_buf;
+  float b1, omb1, b2, omb2, bc1, bc2, aeps, two_alpha, nd, temp;
+  // scalar-divisor reciprocals for BDL_FLAG_RECIP_DIV (host-rounded fl32(1/s64))
+  float inv_s2, inv_nd, inv_ca, inv_cb, inv_temp, inv_bc1, inv_bc2;
 };
+
+// fl32(1/s64) from the caller, or 1/fl32(s) when it left the field 0
+inline float recip_or(float inv, float s) { return inv != 0.0f ? inv : 1.0f / s; }
+
+constexpr int32_t kFlagGradIsMom = 0x1000;  // internal: bdl_adam_args.grad_is_mom
 
 // Scalar division in the reference's rounding: torch CPU divides (x / s);
 // torch on a HIP device multiplies by the fp32 reciprocal (x * fl(1/s)).
@@ -479,10 +491,10 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
   c.grad_ready = (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) && (a.flags & BDL_FLAG_GRAD_READY);
   c.clip = (METHOD == BDL_SGLD) && a.clip != nullptr;
   c.clip_coef = c.clip ? a.clip[1] : 1.0f;
-  c.inv_s2 = 1.0f / a.sigma2;
-  c.inv_nd = 1.0f / a.n_data;
-  c.inv_ca = 1.0f / a.ca;
-  c.inv_cb = 1.0f / a.cb;
+  c.inv_s2 = a.inv_s2;
+  c.inv_nd = a.inv_nd;
+  c.inv_ca = a.inv_ca;
+  c.inv_cb = a.inv_cb;
 
   const int64_t ngroups = (a.n + 3) >> 2;
   const int64_t nfull = a.n >> 2;  // groups entirely inside [0, n)
@@ -526,6 +538,221 @@ __global__ __launch_bounds__(kBlock) void bdl_step_kernel(const KArgs a) {
     step_body<METHOD, NOISE, COLLECT, true, UNROLL>(a);
   else
     step_body<METHOD, NOISE, COLLECT, false, UNROLL>(a);
+}
+
+// ---------------------------------------------------------------------------
+// Adam-preconditioned SGHMC (methods/adam_sghmc.py:500-553,
+// methods/adam_csghmc.py:812-860) + torch.optim.SGD step + running moments.
+// Same sweep as the SG-MCMC step (run table in LDS, branch-free fast path over
+// whole iterations inside one run, guarded slow path elsewhere); the element
+// update carries three more state vectors (v_mom in args.mom, Adam m and v) and
+// optionally the SGD buffer: 40 B/element, 48 with the buffer.
+// ---------------------------------------------------------------------------
+struct AdamConst {
+  bool sgd_mom, sgd_mom_read, has_m2, grad_is_mom;
+  float inv_s2, inv_nd, inv_temp, inv_bc1, inv_bc2, inv_ca, inv_cb;
+};
+
+template <int NOISE, bool RECIP, bool PRIOR, bool GRADONLY>
+__device__ __forceinline__ void adam_core(const KArgs& a, const AdamConst& c, float eta, float& th,
+                                          float& g, float& vm, float& m, float& v, float& buf,
+                                          float th0, float eps) {
+  const float gs = sdiv<RECIP>(g, a.temp, c.inv_temp);  // p.grad / temperature
+  float gU = gs;
+  if constexpr (PRIOR) {
+    const float d = th - th0;
+    const float e = sdiv<RECIP>(d, a.sigma2, c.inv_s2);
+    gU = gs + sdiv<RECIP>(e, a.n_data, c.inv_nd);
+  }
+  m = m * a.b1 + gU * a.omb1;            // beta1*m + (1-beta1)*grad_U
+  v = v * a.b2 + (gU * gU) * a.omb2;     // beta2*v + (1-beta2)*(grad_U*grad_U)
+  const float mh = sdiv<RECIP>(m, a.bc1, c.inv_bc1);
+  const float vh = sdiv<RECIP>(v, a.bc2, c.inv_bc2);
+  const float den = sqrtf(vh) + a.aeps;  // torch.sqrt(v_hat) + eps
+  const float pg = mh / den;             // precond_grad (tensor / tensor: true division)
+  const float pt = 1.0f / den;           // precond_term = 1.0 / (...) = reciprocal() * 1.0
+  float nz = 0.0f;
+  if constexpr (NOISE != BDL_NOISE_NONE) {
+    const float q = sdiv<RECIP>(pt * a.two_alpha, a.n_data, c.inv_nd);
+    nz = (sqrtf(q) * a.nd) * eps;        // nd*sqrt(2a*pt/N) * randn_like
+  }
+  vm = (vm * a.one_minus_alpha + pg * eta) + nz;
+  const float gp = c.grad_is_mom ? vm : g + vm;  // p.grad = v_mom (.clone()) | p.grad + v_mom
+  if constexpr (GRADONLY) {
+    g = gp;
+  } else {
+    float stepv = gp;
+    if (c.sgd_mom) {
+      buf = (a.flags & BDL_FLAG_FIRST_STEP) ? gp : (a.mu * buf + gp);
+      stepv = buf;
+    }
+    th = fmaf(-eta, stepv, th);  // SGD: param.add_(d_p, alpha=-lr)
+  }
+}
+
+template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, bool PRIOR>
+__device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, int64_t gb,
+                                          float eta) {
+  constexpr int U = 2;
+  constexpr bool kReadMoments = (COLLECT == BDL_COLLECT_MEAN);
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+  f4v th[U], g[U], vm[U], m[U], v[U], buf[U], t0[U], ep[U], m1[U], m2[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+    buf[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
+    th[u] = vload(a.theta + e);
+    g[u] = vload(a.grad + e);
+    vm[u] = vload(a.mom + e);
+    m[u] = vload(a.adam_m + e);
+    v[u] = vload(a.adam_v + e);
+    if (!GRADONLY && c.sgd_mom_read) buf[u] = vload(a.sgd_buf + e);
+    if constexpr (PRIOR) t0[u] = vload(a.prior_mean + e);
+    if constexpr (NOISE == BDL_NOISE_BUFFER) ep[u] = vload(a.noise + e);
+    if constexpr (kReadMoments) {
+      m1[u] = vload(a.mom1 + e);
+      if (c.has_m2) m2[u] = vload(a.mom2 + e);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    const int64_t e = gi * 4;
+    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+    StepConst cc;  // collect_core only reads inv_ca / inv_cb
+    cc.inv_ca = c.inv_ca;
+    cc.inv_cb = c.inv_cb;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float xt = th[u][j], xg = g[u][j], xvm = vm[u][j], xm = m[u][j], xv = v[u][j],
+            xb = buf[u][j], x1 = m1[u][j], x2 = m2[u][j];
+      adam_core<NOISE, RECIP, PRIOR, GRADONLY>(a, c, eta, xt, xg, xvm, xm, xv, xb, t0[u][j],
+                                               ep[u][j]);
+      collect_core<COLLECT, RECIP>(a, cc, xt, x1, x2);
+      th[u][j] = xt;
+      g[u][j] = xg;
+      vm[u][j] = xvm;
+      m[u][j] = xm;
+      v[u][j] = xv;
+      buf[u][j] = xb;
+      m1[u][j] = x1;
+      m2[u][j] = x2;
+    }
+    if constexpr (GRADONLY)
+      vstore(a.grad + e, g[u]);
+    else
+      vstore(a.theta + e, th[u]);
+    vstore(a.mom + e, vm[u]);
+    vstore(a.adam_m + e, m[u]);
+    vstore(a.adam_v + e, v[u]);
+    if (!GRADONLY && c.sgd_mom) vstore(a.sgd_buf + e, buf[u]);
+    if constexpr (COLLECT != BDL_COLLECT_NONE) {
+      vstore(a.mom1 + e, m1[u]);
+      if (c.has_m2) vstore(a.mom2 + e, m2[u]);
+    }
+  }
+}
+
+template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY>
+__device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, int64_t gb,
+                                          int64_t gend) {
+  const int64_t n = a.n;
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+  StepConst cc;
+  cc.inv_ca = c.inv_ca;
+  cc.inv_cb = c.inv_cb;
+  for (int u = 0; u < 2; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    if (gi >= gend) continue;
+    const int64_t e = gi * 4;
+    f4v th = ld4(a.theta, e, n), g = ld4(a.grad, e, n), vm = ld4(a.mom, e, n);
+    f4v m = ld4(a.adam_m, e, n), v = ld4(a.adam_v, e, n), t0 = ld4(a.prior_mean, e, n);
+    f4v buf = z, ep = z, m1 = z, m2 = z;
+    if (!GRADONLY && c.sgd_mom_read) buf = ld4(a.sgd_buf, e, n);
+    if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, n);
+    if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+    if (COLLECT == BDL_COLLECT_MEAN) {
+      m1 = ld4(a.mom1, e, n);
+      if (c.has_m2) m2 = ld4(a.mom2, e, n);
+    }
+    for (int j = 0; j < 4; ++j) {
+      if (e + j >= n) break;
+      const uint32_t at = run_attr(find_run_lds(a.nruns, e + j));
+      float xt = th[j], xg = g[j], xvm = vm[j], xm = m[j], xv = v[j], xb = buf[j];
+      float x1 = m1[j], x2 = m2[j];
+      if (!(at & BDL_ATTR_SKIP)) {
+        const float eta = (at & BDL_ATTR_HEAD) ? a.lr1 : a.lr0;
+        if (at & BDL_ATTR_PRIOR)
+          adam_core<NOISE, RECIP, true, GRADONLY>(a, c, eta, xt, xg, xvm, xm, xv, xb, t0[j], ep[j]);
+        else
+          adam_core<NOISE, RECIP, false, GRADONLY>(a, c, eta, xt, xg, xvm, xm, xv, xb, t0[j], ep[j]);
+      }
+      collect_core<COLLECT, RECIP>(a, cc, xt, x1, x2);
+      th[j] = xt;
+      g[j] = xg;
+      vm[j] = xvm;
+      m[j] = xm;
+      v[j] = xv;
+      buf[j] = xb;
+      m1[j] = x1;
+      m2[j] = x2;
+    }
+    if (GRADONLY)
+      st4(a.grad, e, n, g);
+    else
+      st4(a.theta, e, n, th);
+    st4(a.mom, e, n, vm);
+    st4(a.adam_m, e, n, m);
+    st4(a.adam_v, e, n, v);
+    if (!GRADONLY && c.sgd_mom) st4(a.sgd_buf, e, n, buf);
+    if (COLLECT != BDL_COLLECT_NONE) {
+      st4(a.mom1, e, n, m1);
+      if (c.has_m2) st4(a.mom2, e, n, m2);
+    }
+  }
+}
+
+template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY>
+__device__ __forceinline__ void adam_body(const KArgs& a) {
+  AdamConst c;
+  c.sgd_mom = !GRADONLY && (a.flags & BDL_FLAG_MOMENTUM);
+  c.sgd_mom_read = c.sgd_mom && !(a.flags & BDL_FLAG_FIRST_STEP);
+  c.has_m2 = (COLLECT != BDL_COLLECT_NONE) && (a.mom2 != nullptr);
+  c.grad_is_mom = (a.flags & kFlagGradIsMom) != 0;
+  c.inv_s2 = a.inv_s2;
+  c.inv_nd = a.inv_nd;
+  c.inv_temp = a.inv_temp;
+  c.inv_bc1 = a.inv_bc1;
+  c.inv_bc2 = a.inv_bc2;
+  c.inv_ca = a.inv_ca;
+  c.inv_cb = a.inv_cb;
+  constexpr int64_t kIter = (int64_t)kBlock * 2;
+  const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
+  for (int i = threadIdx.x; i < a.nruns; i += kBlock) s_runs[i] = a.runs[i];
+  __syncthreads();
+  int r = find_run_lds(a.nruns, (int64_t)blockIdx.x * kIter * 4);
+  for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {
+    while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
+    const int64_t gend = min(gb + kIter, ngroups);
+    const uint32_t attr = run_attr(r);
+    if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 && !(attr & BDL_ATTR_SKIP)) {
+      const float eta = (attr & BDL_ATTR_HEAD) ? a.lr1 : a.lr0;
+      if (attr & BDL_ATTR_PRIOR)
+        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, true>(a, c, gb, eta);
+      else
+        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, false>(a, c, gb, eta);
+    } else {
+      adam_slow<NOISE, COLLECT, RECIP, GRADONLY>(a, c, gb, gend);
+    }
+  }
+}
+
+template <int NOISE, int COLLECT, bool GRADONLY>
+__global__ __launch_bounds__(kBlock) void bdl_adam_kernel(const KArgs a) {
+  if (a.flags & BDL_FLAG_RECIP_DIV)
+    adam_body<NOISE, COLLECT, true, GRADONLY>(a);
+  else
+    adam_body<NOISE, COLLECT, false, GRADONLY>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -581,8 +808,8 @@ __device__ __forceinline__ void sqnorm_body(const KArgs& a, float* __restrict__ 
   constexpr int64_t kIter = (int64_t)kBlock * 2;
   StepConst c;
   c.sgd_mom = c.sgd_mom_read = c.has_m2 = c.grad_ready = c.clip = false;
-  c.inv_s2 = 1.0f / a.sigma2;
-  c.inv_nd = 1.0f / a.n_data;
+  c.inv_s2 = a.inv_s2;
+  c.inv_nd = a.inv_nd;
   c.inv_ca = c.inv_cb = c.clip_coef = 1.0f;
   const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
   for (int i = threadIdx.x; i < a.nruns; i += kBlock) s_runs[i] = a.runs[i];
@@ -677,12 +904,12 @@ struct MArgs {
   int64_t n;
   int32_t collect;
   int32_t recip;
-  float ca, cb;
+  float ca, cb, inv_ca, inv_cb;
 };
 
 __global__ __launch_bounds__(kBlock) void bdl_moments_kernel(const MArgs a) {
   const int64_t ngroups = (a.n + 3) >> 2;
-  const float inv_ca = 1.0f / a.ca, inv_cb = 1.0f / a.cb;
+  const float inv_ca = a.inv_ca, inv_cb = a.inv_cb;
   for (int64_t gi = (int64_t)blockIdx.x * kBlock + threadIdx.x; gi < ngroups;
        gi += (int64_t)gridDim.x * kBlock) {
     const int64_t e = gi * 4;
@@ -734,7 +961,7 @@ struct SArgs {
   const float* __restrict__ noise;
   int64_t n;
   int32_t var_mode, noise_mode;
-  float ratio, var_floor;
+  float ratio, var_floor, inv_ratio;
   uint64_t seed, chain, step;
 };
 
@@ -760,7 +987,7 @@ __global__ __launch_bounds__(kBlock) void bdl_sample_kernel(const SArgs a) {
       else if (a.var_mode == BDL_VAR_RAW_MOMENTS)
         var = a.ratio * (qj - mj * mj);  // sgld.py:342
       else if (a.var_mode == BDL_VAR_WELFORD)
-        var = qj / a.ratio;  // csghmc.py:455
+        var = a.inv_ratio != 0.0f ? qj * a.inv_ratio : qj / a.ratio;  // csghmc.py:455
       else
         var = qj;
       if (!(var != var)) var = fmaxf(var, a.var_floor);  // clamp_(min=1e-12); NaN stays NaN
@@ -852,6 +1079,32 @@ StepKernel pick_step(int method, int noise, int collect, int unroll) {
   return nullptr;
 }
 
+template <int NOISE>
+StepKernel pick_adam_collect(int collect, bool grad_only) {
+  if (grad_only) return collect == BDL_COLLECT_NONE ? bdl_adam_kernel<NOISE, BDL_COLLECT_NONE, true> : nullptr;
+  switch (collect) {
+    case BDL_COLLECT_NONE:
+      return bdl_adam_kernel<NOISE, BDL_COLLECT_NONE, false>;
+    case BDL_COLLECT_MEAN_INIT:
+      return bdl_adam_kernel<NOISE, BDL_COLLECT_MEAN_INIT, false>;
+    case BDL_COLLECT_MEAN:
+      return bdl_adam_kernel<NOISE, BDL_COLLECT_MEAN, false>;
+  }
+  return nullptr;  // the Adam runners collect running means only
+}
+
+StepKernel pick_adam(int noise, int collect, bool grad_only) {
+  switch (noise) {
+    case BDL_NOISE_NONE:
+      return pick_adam_collect<BDL_NOISE_NONE>(collect, grad_only);
+    case BDL_NOISE_BUFFER:
+      return pick_adam_collect<BDL_NOISE_BUFFER>(collect, grad_only);
+    case BDL_NOISE_PHILOX:
+      return pick_adam_collect<BDL_NOISE_PHILOX>(collect, grad_only);
+  }
+  return nullptr;
+}
+
 int grid_for(int64_t ngroups, int per_block_groups) {
   const int64_t want = (ngroups + per_block_groups - 1) / per_block_groups;
   const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
@@ -932,6 +1185,10 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   a.chain = s->chain;
   a.step = s->step;
   a.clip = clip;
+  a.inv_s2 = recip_or(s->inv_sigma2, s->sigma2);
+  a.inv_nd = recip_or(s->inv_n_data, s->n_data);
+  a.inv_ca = recip_or(s->inv_collect_a, s->collect_a);
+  a.inv_cb = recip_or(s->inv_collect_b, s->collect_b);
 
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kBlock), (size_t)s->nruns * sizeof(bdl_run),
                      stream, a);
@@ -1044,6 +1301,8 @@ int bdl_sgld_step_clipped(const bdl_step_args* s, float max_norm, void* workspac
   a.seed = s->seed;
   a.chain = s->chain;
   a.step = s->step;
+  a.inv_s2 = recip_or(s->inv_sigma2, s->sigma2);
+  a.inv_nd = recip_or(s->inv_n_data, s->n_data);
   const int64_t ngroups = (s->n + 3) / 4;
   const int64_t iters = (ngroups + 2 * kBlock - 1) / (2 * kBlock);
   const int64_t cap = std::min<int64_t>((int64_t)device_cu_count() * g_blocks_per_cu, kMaxNormPartials);
@@ -1069,6 +1328,94 @@ int bdl_sgld_step_clipped(const bdl_step_args* s, float max_norm, void* workspac
   return launch_step(s, ws, st);
 }
 
+int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream) {
+  if (!s || !ad) return fail(BDL_ERR_NULL, "bdl_adam_step: null args");
+  if (s->method != BDL_ADAM_SGHMC && s->method != BDL_ADAM_SGHMC_GRAD)
+    return fail(BDL_ERR_ARG, "bdl_adam_step: method must be BDL_ADAM_SGHMC or BDL_ADAM_SGHMC_GRAD");
+  if (s->noise_mode < BDL_NOISE_NONE || s->noise_mode > BDL_NOISE_PHILOX)
+    return fail(BDL_ERR_ARG, "bdl_adam_step: unknown noise mode");
+  if (s->collect < BDL_COLLECT_NONE || s->collect > BDL_COLLECT_MEAN)
+    return fail(BDL_ERR_ARG, "bdl_adam_step: unknown collect mode");
+  if (s->n < 0) return fail(BDL_ERR_ARG, "bdl_adam_step: n < 0");
+  if (s->n == 0) return BDL_OK;
+  const bool grad_only = s->method == BDL_ADAM_SGHMC_GRAD;
+  if (!s->theta || !s->grad || !s->mom || !s->prior_mean || !ad->adam_m || !ad->adam_v ||
+      !s->runs || s->nruns < 1)
+    return fail(BDL_ERR_NULL, "bdl_adam_step: theta, grad, mom, prior_mean, adam_m, adam_v and runs are required");
+  if (s->nruns > kMaxRuns)
+    return fail(BDL_ERR_RUNS, "bdl_adam_step: more than 4096 runs (merge parameter groups)");
+  if (!grad_only && (s->flags & BDL_FLAG_MOMENTUM) && !ad->sgd_buf)
+    return fail(BDL_ERR_NULL, "bdl_adam_step: sgd_buf is required with BDL_FLAG_MOMENTUM");
+  if (s->noise_mode == BDL_NOISE_BUFFER && !s->noise)
+    return fail(BDL_ERR_NULL, "bdl_adam_step: noise buffer is required");
+  if (s->collect != BDL_COLLECT_NONE && !s->mom1)
+    return fail(BDL_ERR_NULL, "bdl_adam_step: mom1 is required to collect");
+  if (s->flags & BDL_FLAG_GRAD_READY)
+    return fail(BDL_ERR_ARG, "bdl_adam_step: GRAD_READY is not an Adam flag (use bdl_sgmcmc_step)");
+  const void* ptrs[] = {s->theta, s->grad, s->mom, s->prior_mean, s->noise, s->mom1, s->mom2,
+                        ad->adam_m, ad->adam_v, ad->sgd_buf};
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_adam_step: vector not 16-B aligned");
+  StepKernel k = pick_adam(s->noise_mode, s->collect, grad_only);
+  if (!k) return fail(BDL_ERR_ARG, "bdl_adam_step: unsupported noise/collect combination");
+
+  KArgs a{};
+  a.theta = s->theta;
+  a.grad = s->grad;
+  a.mom = s->mom;
+  a.prior_mean = s->prior_mean;
+  a.noise = s->noise;
+  a.mom1 = s->mom1;
+  a.mom2 = s->mom2;
+  a.runs = s->runs;
+  a.nruns = s->nruns;
+  a.flags = (s->flags & ~kFlagGradIsMom) | (ad->grad_is_mom ? kFlagGradIsMom : 0);
+  a.n = s->n;
+  a.lr0 = s->lr[0];
+  a.lr1 = s->lr[1];
+  a.one_minus_alpha = s->one_minus_alpha;
+  a.sigma2 = s->sigma2;
+  a.n_data = s->n_data;
+  a.mu = s->mu;
+  a.ca = s->collect_a;
+  a.cb = s->collect_b;
+  a.seed = s->seed;
+  a.chain = s->chain;
+  a.step = s->step;
+  a.adam_m = ad->adam_m;
+  a.adam_v = ad->adam_v;
+  a.sgd_buf = ad->sgd_buf;
+  a.b1 = ad->beta1;
+  a.omb1 = ad->one_minus_beta1;
+  a.b2 = ad->beta2;
+  a.omb2 = ad->one_minus_beta2;
+  a.bc1 = ad->bias_corr1;
+  a.bc2 = ad->bias_corr2;
+  a.aeps = ad->eps;
+  a.two_alpha = ad->two_alpha;
+  a.nd = ad->nd;
+  a.temp = ad->temperature;
+  a.inv_s2 = recip_or(s->inv_sigma2, s->sigma2);
+  a.inv_nd = recip_or(s->inv_n_data, s->n_data);
+  a.inv_ca = recip_or(s->inv_collect_a, s->collect_a);
+  a.inv_cb = recip_or(s->inv_collect_b, s->collect_b);
+  a.inv_temp = recip_or(ad->inv_temperature, ad->temperature);
+  a.inv_bc1 = recip_or(ad->inv_bias_corr1, ad->bias_corr1);
+  a.inv_bc2 = recip_or(ad->inv_bias_corr2, ad->bias_corr2);
+  const int64_t ngroups = (s->n + 3) / 4;
+  const int64_t iters = (ngroups + 2 * kBlock - 1) / (2 * kBlock);
+  const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
+  const int grid = (int)std::max<int64_t>(1, std::min(iters, cap));
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), (size_t)s->nruns * sizeof(bdl_run),
+                     (hipStream_t)stream, a);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    g_last_error = std::string("bdl_adam_step: launch failed: ") + hipGetErrorString(err);
+    return BDL_ERR_LAUNCH;
+  }
+  return BDL_OK;
+}
+
 int bdl_moments_update(const bdl_moments_args* m, void* stream) {
   if (!m) return fail(BDL_ERR_NULL, "bdl_moments_update: null args");
   if (m->n < 0 || m->collect < BDL_COLLECT_WELFORD_INIT || m->collect > BDL_COLLECT_MEAN)
@@ -1079,7 +1426,8 @@ int bdl_moments_update(const bdl_moments_args* m, void* stream) {
   for (const void* p : ptrs)
     if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_moments_update: vector not 16-B aligned");
   MArgs a{m->theta, m->mom1, m->mom2, m->n, m->collect, (m->flags & BDL_FLAG_RECIP_DIV) ? 1 : 0,
-          m->collect_a, m->collect_b};
+          m->collect_a, m->collect_b, recip_or(m->inv_collect_a, m->collect_a),
+          recip_or(m->inv_collect_b, m->collect_b)};
   hipLaunchKernelGGL(bdl_moments_kernel, dim3(grid_for((m->n + 3) / 4, kBlock * 4)), dim3(kBlock), 0,
                      (hipStream_t)stream, a);
   const hipError_t err = hipGetLastError();
@@ -1102,7 +1450,7 @@ int bdl_posterior_sample(const bdl_sample_args* s, void* stream) {
   for (const void* p : ptrs)
     if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_posterior_sample: vector not 16-B aligned");
   SArgs a{s->out, s->mom1, s->mom2, s->noise, s->n, s->var_mode, s->noise_mode,
-          s->ratio, s->var_floor, s->seed, s->chain, s->step};
+          s->ratio, s->var_floor, s->inv_ratio, s->seed, s->chain, s->step};
   hipLaunchKernelGGL(bdl_sample_kernel, dim3(grid_for((s->n + 3) / 4, kBlock * 4)), dim3(kBlock), 0,
                      (hipStream_t)stream, a);
   const hipError_t err = hipGetLastError();

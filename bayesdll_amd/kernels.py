@@ -26,14 +26,24 @@ def _div_flag(div_mode=None):
     return L.FLAG_RECIP_DIV if (div_mode or DIV_MODE) == "recip" else 0
 
 
+def _inv(s):
+    """fl32(1/s) of the float64 divisor s: torch on a HIP device forms the
+    reciprocal of a Python-scalar divisor in double and multiplies by it
+    (tools/div_probe.py); ctypes does the final fp32 rounding."""
+    s = float(s)
+    return 1.0 / s if s != 0.0 else 0.0
+
+
 def _step_args(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1.0,
                prior_sig=0.0, sigma2=1.0, n_data=1.0, mu=0.0, first_step=False,
                momentum=False, collect=L.COLLECT_NONE, mom1=None, mom2=None, collect_a=1.0,
-               collect_b=1.0, seed=0, chain=0, step=0, div_mode=None, noise=None, grad_ready=False):
+               collect_b=1.0, seed=0, chain=0, step=0, div_mode=None, noise=None, grad_ready=False,
+               mom_buf=None):
     a = L.StepArgs()
     a.theta = state.theta.data_ptr()
     a.grad = state.grad.data_ptr()
-    a.mom = None if state.mom is None else state.mom.data_ptr()
+    mb = state.mom if mom_buf is None else mom_buf  # mom_buf: a separate SGD buffer
+    a.mom = None if mb is None else mb.data_ptr()
     a.prior_mean = None if state.prior is None else state.prior.data_ptr()
     nz = noise if noise is not None else state.noise
     a.noise = None if nz is None else nz.data_ptr()
@@ -56,6 +66,8 @@ def _step_args(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1
     a.mu = float(mu)
     a.collect_a = float(collect_a)
     a.collect_b = float(collect_b)
+    a.inv_sigma2, a.inv_n_data = _inv(sigma2), _inv(n_data)
+    a.inv_collect_a, a.inv_collect_b = _inv(collect_a), _inv(collect_b)
     a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     a.chain = int(chain) & 0xFFFFFFFFFFFFFFFF
     a.step = int(step) & 0xFFFFFFFFFFFFFFFF
@@ -66,6 +78,38 @@ def sgmcmc_step(state, method, **kw):
     """One fused update over `state` (a FlatState). Asynchronous."""
     a = _step_args(state, method, **kw)
     L.check(L.lib().bdl_sgmcmc_step(a, L.current_stream_handle(state.device)), "bdl_sgmcmc_step")
+
+
+def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps, t,
+              momentum_decay, nd, temperature=1.0, grad_is_mom=False, lrs, noise_mode,
+              sigma2, n_data, mu=0.0, first_step=False, momentum=False, collect=L.COLLECT_NONE,
+              mom1=None, mom2=None, collect_a=1.0, collect_b=1.0, seed=0, chain=0, step=0,
+              div_mode=None, noise=None):
+    """One fused Adam-preconditioned SGHMC step (methods/adam_sghmc.py:500-553,
+    adam_csghmc.py:812-860) + SGD step.  The host-side scalars are formed in
+    float64 exactly as the reference's Python does (1 - beta1, 1 - beta1**t,
+    2 * momentum_decay, 1 - momentum_decay); ctypes rounds them to fp32."""
+    a = _step_args(state, method, lrs=lrs, noise_scale=(0.0, 0.0), noise_mode=noise_mode,
+                   one_minus_alpha=1 - momentum_decay, sigma2=sigma2, n_data=n_data, mu=mu,
+                   first_step=first_step, momentum=momentum, collect=collect, mom1=mom1,
+                   mom2=mom2, collect_a=collect_a, collect_b=collect_b, seed=seed, chain=chain,
+                   step=step, div_mode=div_mode, noise=noise)
+    ad = L.AdamArgs()
+    ad.adam_m = adam_m.data_ptr()
+    ad.adam_v = adam_v.data_ptr()
+    ad.sgd_buf = None if sgd_buf is None else sgd_buf.data_ptr()
+    ad.beta1, ad.one_minus_beta1 = float(beta1), 1 - float(beta1)
+    ad.beta2, ad.one_minus_beta2 = float(beta2), 1 - float(beta2)
+    bc1, bc2 = 1 - float(beta1) ** int(t), 1 - float(beta2) ** int(t)
+    ad.bias_corr1, ad.bias_corr2 = bc1, bc2
+    ad.eps = float(eps)
+    ad.two_alpha = 2 * float(momentum_decay)
+    ad.nd = float(nd)
+    ad.temperature = float(temperature)
+    ad.inv_bias_corr1, ad.inv_bias_corr2 = _inv(bc1), _inv(bc2)
+    ad.inv_temperature = _inv(temperature)
+    ad.grad_is_mom = 1 if grad_is_mom else 0
+    L.check(L.lib().bdl_adam_step(a, ad, L.current_stream_handle(state.device)), "bdl_adam_step")
 
 
 def clip_workspace(state):
@@ -102,12 +146,13 @@ def moments_update(theta, mom1, mom2, collect, collect_a=1.0, collect_b=1.0, div
     a.collect = int(collect)
     a.flags = _div_flag(div_mode)
     a.collect_a, a.collect_b = float(collect_a), float(collect_b)
+    a.inv_collect_a, a.inv_collect_b = _inv(collect_a), _inv(collect_b)
     L.check(L.lib().bdl_moments_update(a, L.current_stream_handle(theta.device)),
             "bdl_moments_update")
 
 
 def posterior_sample(out, mom1, mom2, *, var_mode, ratio=1.0, var_floor=1e-12, noise=None,
-                     seed=0, chain=0, step=0):
+                     seed=0, chain=0, step=0, div_mode=None):
     """out = mom1 + sqrt(clamp(var(mom1, mom2), var_floor)) * eps (eps: buffer or Philox)."""
     L.require_hip(out, "out")
     a = L.SampleArgs()
@@ -119,6 +164,8 @@ def posterior_sample(out, mom1, mom2, *, var_mode, ratio=1.0, var_floor=1e-12, n
     a.noise_mode = L.NOISE_BUFFER if noise is not None else L.NOISE_PHILOX
     a.ratio = float(ratio)
     a.var_floor = float(var_floor)
+    # WELFORD M2 / (n-1): torch-on-GPU multiplies by the reciprocal
+    a.inv_ratio = _inv(ratio) if _div_flag(div_mode) else 0.0
     a.seed, a.chain, a.step = int(seed), int(chain), int(step) & 0xFFFFFFFFFFFFFFFF
     L.check(L.lib().bdl_posterior_sample(a, L.current_stream_handle(out.device)),
             "bdl_posterior_sample")

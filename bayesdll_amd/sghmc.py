@@ -32,6 +32,18 @@ class Runner(_SGLDRunner):
     def _momentum(args):
         return 0
 
+    def _extra_ckpt(self):
+        """methods/sghmc.py:382: 'momentum_buffer' (name -> v) is saved too."""
+        return {"momentum_buffer": {k: v.detach().clone()
+                                    for k, v in self.model.momentum_buffer.items()}}
+
+    def _load_extra(self, ckpt):
+        """methods/sghmc.py:400-401."""
+        mb = ckpt.get("momentum_buffer")
+        if mb:
+            self._state()  # bind the flat state first
+            self.model.load_momentum_buffer(mb)
+
 
 class Model(FusedModelBase):
     """SGHMC sampler step (methods/sghmc.py:409-512), fused on device."""

@@ -43,13 +43,24 @@ class FusedSGD:
         g = self.optimizer.param_groups
         return (g[0]["lr"], g[1]["lr"] if len(g) > 1 else g[0]["lr"])
 
-    def export_state(self, state):
-        """Expose the flat momentum buffer as the optimizer's per-param
-        momentum_buffer (so optimizer.state_dict() matches torch's layout)."""
+    def export_state(self, state, buf=None):
+        """Expose the flat momentum buffer (state.mom, or `buf`) as the
+        optimizer's per-param momentum_buffer (so optimizer.state_dict()
+        matches torch's layout)."""
         if self.momentum == 0 or not self.has_buffer:
             return
-        for p, v in zip(state.params, state.views(state.mom)):
+        for p, v in zip(state.params, state.views(state.mom if buf is None else buf)):
             self.optimizer.state[p]["momentum_buffer"] = v
+
+    def import_state(self, state, buf=None):
+        """Inverse of export_state after optimizer.load_state_dict()."""
+        bufs = [self.optimizer.state.get(p, {}).get("momentum_buffer") for p in state.params]
+        dst = state.mom if buf is None else buf
+        if dst is not None and bufs and all(b is not None for b in bufs):
+            with torch.no_grad():
+                for v, b in zip(state.views(dst), bufs):
+                    v.copy_(b)
+            self.has_buffer = True
 
 
 class Runner:
@@ -192,13 +203,14 @@ class Runner:
     def save_ckpt(self, epoch):
         """methods/sgld.py:367-385 — same file name and keys."""
         fname = os.path.join(self.args.log_dir, "ckpt.pt")
-        self.sgd.export_state(self._state())
+        self._export_sgd()
         torch.save({"last_theta": self.net.state_dict(),
                     "post_theta_mom1": self.post_theta_mom1,
                     "post_theta_mom2": self.post_theta_mom2 if self.nst > 0 else None,
                     "post_theta_cnt": self.post_theta_cnt,
                     "prior_sig": self.model.prior_sig,
                     "optimizer": self.optimizer.state_dict(),
+                    **self._extra_ckpt(),
                     "epoch": epoch}, fname)
         return fname
 
@@ -213,14 +225,18 @@ class Runner:
         self.post_theta_cnt = ckpt["post_theta_cnt"] if exact_count else ckpt["epoch"]
         self.model.prior_sig = ckpt["prior_sig"]
         self.optimizer.load_state_dict(ckpt["optimizer"])
-        st = self._state()
-        bufs = [self.optimizer.state.get(p, {}).get("momentum_buffer") for p in st.params]
-        if st.mom is not None and all(b is not None for b in bufs):
-            with torch.no_grad():
-                for v, b in zip(st.views(st.mom), bufs):
-                    v.copy_(b)
-            self.sgd.has_buffer = True
+        self._load_extra(ckpt)
         return ckpt["epoch"]
+
+    # checkpoint hooks: SGLD's flat state.mom is the SGD momentum buffer
+    def _export_sgd(self):
+        self.sgd.export_state(self._state())
+
+    def _extra_ckpt(self):
+        return {}
+
+    def _load_extra(self, ckpt):
+        self.sgd.import_state(self._state())
 
 
 class Model(FusedModelBase):

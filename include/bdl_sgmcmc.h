@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define BDL_ABI_VERSION 1
+#define BDL_ABI_VERSION 2
 
 typedef enum bdl_status {
   BDL_OK = 0,
@@ -73,7 +73,10 @@ typedef enum bdl_method {
   BDL_SGHMC = 1,       /* methods/sghmc.py:482-510 + SGD(momentum 0) step     */
   BDL_SGLD = 2,        /* methods/sgld.py:469-484 (and csgld) + SGD(mu) step  */
   BDL_SGHMC_GRAD = 3,  /* sghmc Model.forward only: grad <- g + v', mom <- v' */
-  BDL_SGLD_GRAD = 4    /* sgld Model.forward only: grad <- g + prior + noise  */
+  BDL_SGLD_GRAD = 4,   /* sgld Model.forward only: grad <- g + prior + noise  */
+  BDL_ADAM_SGHMC = 5,  /* Adam-preconditioned SGHMC + SGD step (bdl_adam_step only):
+                          methods/adam_sghmc.py:500-553 and adam_csghmc.py:812-860 */
+  BDL_ADAM_SGHMC_GRAD = 6 /* its Model.forward only: grad, v_mom, m, v written    */
 } bdl_method;
 
 typedef enum bdl_noise_mode {
@@ -147,11 +150,50 @@ typedef struct bdl_step_args {
   float mu;                /* SGD momentum                                          */
   float collect_a;         /* WELFORD: n; MEAN: multiplier of the old moment        */
   float collect_b;         /* MEAN: divisor                                          */
+  /* Reciprocals of the scalar divisors, fl32(1/s) of the host's float64 s: what
+   * torch on a HIP device multiplies by for tensor / Python-scalar (used with
+   * BDL_FLAG_RECIP_DIV; 0 means 1.0f/fl32(s)). */
+  float inv_sigma2;
+  float inv_n_data;
+  float inv_collect_a;
+  float inv_collect_b;
   float pad1;
   uint64_t seed;           /* Philox key                                            */
   uint64_t chain;          /* chain id (rank)                                        */
   uint64_t step;           /* global step counter                                    */
 } bdl_step_args;
+
+/* Extra state and scalars of the Adam-preconditioned SGHMC step.  Per element,
+ * in the reference's op order (every op separately rounded; "/s" is a scalar
+ * division, rounded per BDL_FLAG_RECIP_DIV):
+ *   gs  = g / temperature                     (adam_csghmc.py:834; 1.0 for adam_sghmc)
+ *   gU  = gs + (theta - theta0)/sigma2/N      (uninformative bias: gs)
+ *   m   = m*beta1 + gU*(1-beta1);   v = v*beta2 + (gU*gU)*(1-beta2)
+ *   d   = sqrt(v/bias_corr2) + eps;  pg = (m/bias_corr1) / d;  pt = 1/d
+ *   vm  = (vm*(1-alpha) + pg*lr) + (sqrt(pt*two_alpha/N)*nd) * eps
+ *   grad = grad_is_mom ? vm : g + vm          (adam_csghmc.py:860 / adam_sghmc.py:553)
+ *   then torch.optim.SGD (momentum mu, buffer sgd_buf) steps theta with grad.
+ * bdl_step_args supplies theta, grad, prior_mean, noise, runs, lr, one_minus_alpha
+ * (= fl32(1 - momentum_decay)), sigma2, n_data, mu, flags, collect, Philox key;
+ * args->mom is v_mom (Model.momentum_buffer). */
+typedef struct bdl_adam_args {
+  float* adam_m;           /* Model.m (first moment)                                */
+  float* adam_v;           /* Model.v (second moment)                               */
+  float* sgd_buf;          /* SGD momentum buffer; required iff BDL_FLAG_MOMENTUM   */
+  float beta1, one_minus_beta1, beta2, one_minus_beta2;
+  float bias_corr1;        /* fl32(1 - beta1**t)                                    */
+  float bias_corr2;        /* fl32(1 - beta2**t)                                    */
+  float eps;               /* Adam epsilon                                          */
+  float two_alpha;         /* fl32(2 * momentum_decay)                              */
+  float nd;                /* noise discount                                        */
+  float temperature;       /* adam_csghmc temperature (1.0 otherwise)               */
+  float inv_bias_corr1;    /* reciprocals as in bdl_step_args.inv_* (0 -> 1/fl32(s)) */
+  float inv_bias_corr2;
+  float inv_temperature;
+  float pad2;
+  int32_t grad_is_mom;     /* 1: p.grad = v_mom (adam_csghmc); 0: g + v_mom         */
+  int32_t pad;
+} bdl_adam_args;
 
 /* Stand-alone posterior-moment update (no parameter update). */
 typedef struct bdl_moments_args {
@@ -163,6 +205,8 @@ typedef struct bdl_moments_args {
   int32_t flags;           /* BDL_FLAG_RECIP_DIV */
   float collect_a;
   float collect_b;
+  float inv_collect_a;     /* see bdl_step_args.inv_*                                 */
+  float inv_collect_b;
 } bdl_moments_args;
 
 /* Variance form used by bdl_posterior_sample. */
@@ -182,6 +226,8 @@ typedef struct bdl_sample_args {
   int32_t noise_mode;      /* BDL_NOISE_BUFFER or BDL_NOISE_PHILOX                    */
   float ratio;             /* RAW_MOMENTS multiplier / WELFORD divisor                */
   float var_floor;         /* clamp_(min=...) — 1e-12 in the reference                 */
+  float inv_ratio;         /* WELFORD: nonzero -> multiply by it (torch-on-GPU rounding) */
+  float pad;
   uint64_t seed, chain, step;
 } bdl_sample_args;
 
@@ -217,6 +263,13 @@ int bdl_moments_update(const bdl_moments_args* args, void* hip_stream);
 int64_t bdl_clip_workspace_bytes(int64_t n);
 int bdl_sgld_step_clipped(const bdl_step_args* args, float max_norm, void* workspace,
                           void* hip_stream);
+
+/* One fused Adam-preconditioned SGHMC step: replaces the per-tensor loop of
+ * methods/adam_sghmc.py:500-553 / adam_csghmc.py:812-860 and the following
+ * optimizer.step().  args->method: BDL_ADAM_SGHMC (update + SGD step, collect
+ * NONE / MEAN_INIT / MEAN) or BDL_ADAM_SGHMC_GRAD (grad, v_mom, m, v only).
+ * 40 B/element (theta, v_mom, m, v r/w; g, theta0 r), +8 with an SGD buffer. */
+int bdl_adam_step(const bdl_step_args* args, const bdl_adam_args* adam, void* hip_stream);
 
 /* theta_s = mean + sqrt(clamp(var)) * eps. */
 int bdl_posterior_sample(const bdl_sample_args* args, void* hip_stream);

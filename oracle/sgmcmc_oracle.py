@@ -128,6 +128,36 @@ def sgld_model(params, params0, grads, names, readout, lrs, prior_sig, bias, N, 
     return out
 
 
+def adam_sghmc_model(params, params0, grads, vms, ms, vs, names, readout, lrs, prior_sig, bias,
+                     alpha, beta1, beta2, eps, t, N, nd, noise, temperature=1.0,
+                     grad_is_mom=False):
+    """methods/adam_sghmc.py:512-553 (grad_is_mom=False, temperature 1) and
+    methods/adam_csghmc.py:819-860 (grad_is_mom=True, g / temperature).
+    Returns (new .grad list, v_mom list, m list, v list); the reference rebinds
+    its dict entries, so the inputs are not modified."""
+    out_g, out_vm, out_m, out_v = [], [], [], []
+    for nm, p, p0, g, vm, m, v, e in zip(names, params, params0, grads, vms, ms, vs, noise):
+        lr = lrs[1] if readout in nm else lrs[0]
+        gs = g / temperature
+        if "bias" in nm and bias == "uninformative":
+            gU = gs
+        else:
+            gU = gs + (p - p0) / (prior_sig ** 2) / N
+        m = beta1 * m + (1 - beta1) * gU
+        v = beta2 * v + (1 - beta2) * (gU * gU)
+        m_hat = m / (1 - beta1 ** t)
+        v_hat = v / (1 - beta2 ** t)
+        precond_grad = m_hat / (torch.sqrt(v_hat) + eps)
+        precond_term = 1.0 / (torch.sqrt(v_hat) + eps)
+        ns = nd * torch.sqrt(2 * alpha * precond_term / N)
+        vm = vm * (1 - alpha) + lr * precond_grad + ns * e
+        out_g.append(vm.clone() if grad_is_mom else g + vm.clone())
+        out_vm.append(vm)
+        out_m.append(m)
+        out_v.append(v)
+    return out_g, out_vm, out_m, out_v
+
+
 def sgd_step(params, grads, bufs, lrs_per_param, momentum):
     """torch.optim.SGD (weight_decay 0, dampening 0, no nesterov), single-tensor."""
     new_bufs = []
@@ -226,10 +256,24 @@ def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
     def noise_now(t):
         return _split(noise_fn(t), shapes)
 
-    if method in ("csghmc", "csgld"):
+    adam = method in ("adam_sghmc", "adam_csghmc")
+    if adam:
+        b1, b2 = float(hp.get("beta1", 0.9)), float(hp.get("beta2", 0.999))
+        aeps = float(hp.get("epsilon", 1e-8))
+        temp = float(hp.get("temperature", 1.0)) if method == "adam_csghmc" else 1.0
+        am = [torch.zeros_like(p) for p in params]
+        av = [torch.zeros_like(p) for p in params]
+        at = 0
+        rec.update(adam_m=[], adam_v=[])
+
+    def adam_rec():
+        rec["adam_m"].append(_cat(am))
+        rec["adam_v"].append(_cat(av))
+
+    if method in ("csghmc", "csgld", "adam_csghmc"):
         sched = CyclicalSchedule(lr0, cfg.get("num_cycles", 10), epochs, cfg.get("beta", 0.5))
         alpha = float(hp.get("momentum_decay", 0.0))
-        moms = [torch.zeros_like(p) for p in params]  # csghmc momentum
+        moms = [torch.zeros_like(p) for p in params]  # csghmc / adam momentum
         bufs = [None] * len(params)                    # csgld SGD buffers
         m1, m2, spc = {}, {}, {}
         samples_collected, current_cycle = 0, 0
@@ -247,6 +291,17 @@ def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
                     rec["mom"].append(_cat(moms))
                     moms = csghmc_update(params, g, moms, names, readout, lrs, prior_sig, alpha, N,
                                          nd, ss, eps)
+                elif adam:  # adam_csghmc.py:312-322: Model, clip, SGD(momentum 0)
+                    rec["mom"].append(_cat(moms))
+                    adam_rec()
+                    at += 1
+                    newg, moms, am, av = adam_sghmc_model(
+                        params, params0, g, moms, am, av, names, readout, lrs, prior_sig, bias,
+                        alpha, b1, b2, aeps, at, N, nd, eps, temperature=temp, grad_is_mom=True)
+                    if cfg.get("clip_grad") is not None:
+                        clip_grad_norm(newg, cfg["clip_grad"])
+                    sgd_step(params, newg, [None] * len(params),
+                             [lrs[1] if h else lrs[0] for h in is_head], 0.0)
                 else:
                     rec["mom"].append(_cat([torch.zeros_like(p) if bb is None else bb
                                             for p, bb in zip(params, bufs)]))
@@ -261,6 +316,7 @@ def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
                     c = sched.get_cycle_number(ep, b, bpe)
                     tv = torch.cat([p.reshape(-1) for p in params])
                     if method == "csghmc":  # Welford, csghmc.py:333-348 (Q2)
+                        # (adam_csghmc.py:345-357 keeps csgld's running means)
                         if c not in m1:
                             m1[c] = tv.clone()
                             m2[c] = torch.zeros_like(tv)
@@ -283,11 +339,18 @@ def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
                     samples_collected += 1
                     spc[c] = spc.get(c, 0) + 1
                 if last:
+                    if adam:  # adam_csghmc.py:372-378 (and :403 again on a new cycle)
+                        moms = [torch.zeros_like(p) for p in params]
+                        am = [torch.zeros_like(p) for p in params]
+                        av = [torch.zeros_like(p) for p in params]
+                        at = 0
                     c = sched.get_cycle_number(ep, b, bpe)
                     if c > current_cycle:
                         current_cycle = c
         rec["theta"].append(_cat(params))
-        rec["mom"].append(_cat(moms) if method == "csghmc" else
+        if adam:
+            adam_rec()
+        rec["mom"].append(_cat(moms) if method in ("csghmc", "adam_csghmc") else
                           _cat([torch.zeros_like(p) if bb is None else bb
                                 for p, bb in zip(params, bufs)]))
         cycles = sorted(m1.keys())
@@ -302,7 +365,7 @@ def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
 
     # sgld / sghmc: burn-in, then running moments every `thin` global iterations
     burnin = int(hp["burnin"])
-    momentum = cfg.get("momentum", 0.0) if method == "sgld" else 0.0
+    momentum = cfg.get("momentum", 0.0) if method in ("sgld", "adam_sghmc") else 0.0
     alpha = float(hp.get("momentum_decay", 0.0))
     moms = [torch.zeros_like(p) for p in params]
     bufs = [None] * len(params)
@@ -328,6 +391,15 @@ def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
                 rec["mom"].append(_cat(moms))
                 newg, moms = sghmc_model(params, params0, g, moms, names, readout, lrs, prior_sig,
                                          bias, alpha, N, nd, eps)
+            elif adam:  # adam_sghmc.py:458-553, then SGD(args.momentum) (:60, :229)
+                rec["mom"].append(_cat(moms))
+                adam_rec()
+                rec.setdefault("sgd_buf", []).append(_cat([torch.zeros_like(p) if bb is None
+                                                           else bb for p, bb in zip(params, bufs)]))
+                at += 1
+                newg, moms, am, av = adam_sghmc_model(
+                    params, params0, g, moms, am, av, names, readout, lrs, prior_sig, bias, alpha,
+                    b1, b2, aeps, at, N, nd, eps)
             else:
                 rec["mom"].append(_cat([torch.zeros_like(p) if bb is None else bb
                                         for p, bb in zip(params, bufs)]))
@@ -343,7 +415,11 @@ def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
                     m2 = (tv ** 2 + cnt * m2) / (cnt + 1)
                 cnt += 1
     rec["theta"].append(_cat(params))
-    rec["mom"].append(_cat(moms) if method == "sghmc" else
+    if adam:
+        adam_rec()
+        rec["sgd_buf"].append(_cat([torch.zeros_like(p) if bb is None else bb
+                                    for p, bb in zip(params, bufs)]))
+    rec["mom"].append(_cat(moms) if method in ("sghmc", "adam_sghmc") else
                       _cat([torch.zeros_like(p) if bb is None else bb
                             for p, bb in zip(params, bufs)]))
     out = {k: np.array(v) for k, v in rec.items()}
@@ -364,6 +440,6 @@ def csghmc_step_cpu(params, grads, moms, names, readout, lrs, prior_sig, momentu
 
 
 __all__ = ["CyclicalSchedule", "csghmc_update", "sghmc_model", "sgld_model", "sgd_step",
-           "clip_grad_norm",
+           "clip_grad_norm", "adam_sghmc_model",
            "posterior_variance_raw", "posterior_variance_welford", "posterior_sample", "simulate",
            "csghmc_step_cpu"]

@@ -48,6 +48,8 @@ def import_reference():
         sys.modules["torchvision." + sub] = m
     sys.modules["torchvision"] = tv
     sys.path[:0] = [REF, os.path.join(REF, "src")]
+    import methods.adam_csghmc
+    import methods.adam_sghmc
     import methods.csghmc
     import methods.csgld
     import methods.cyclical
@@ -115,12 +117,14 @@ def run_method(methods, method, cfg):
     runner = mod.Runner(net, net0, args, logger)
     model_cls = mod.Model
 
-    rec = dict(lrs=[], should_sample=[], theta=[], mom=[], noise=[])
+    adam = method.startswith("adam_")
+    rec = dict(lrs=[], should_sample=[], theta=[], mom=[], noise=[], adam_m=[], adam_v=[],
+               sgd_buf=[])
     cap = Capture()
     orig_forward = model_cls.forward
 
     def state_mom():
-        if method in ("csghmc", "sghmc"):
+        if method in ("csghmc", "sghmc", "adam_sghmc", "adam_csghmc"):
             if not hasattr(runner.model, "momentum_buffer"):
                 return np.zeros(n, np.float32)
             return torch.cat([runner.model.momentum_buffer[nm].reshape(-1)
@@ -132,11 +136,31 @@ def run_method(methods, method, cfg):
             bufs.append(np.zeros(p.numel(), np.float32) if b is None else b.reshape(-1).numpy())
         return np.concatenate(bufs).astype(np.float32)
 
+    def adam_state(attr):
+        d = getattr(runner.model, attr, None)
+        if not isinstance(d, dict):
+            return np.zeros(n, np.float32)
+        return torch.cat([d[nm].reshape(-1) for nm, _ in runner.net.named_parameters()]).numpy().copy()
+
+    def sgd_bufs():
+        bufs = []
+        for p in runner.net.parameters():
+            b = runner.optimizer.state.get(p, {}).get("momentum_buffer")
+            bufs.append(np.zeros(p.numel(), np.float32) if b is None else b.reshape(-1).numpy())
+        return np.concatenate(bufs).astype(np.float32)
+
+    def record_state():
+        rec["mom"].append(state_mom())
+        if adam:
+            rec["adam_m"].append(adam_state("m"))
+            rec["adam_v"].append(adam_state("v"))
+            rec["sgd_buf"].append(sgd_bufs())
+
     def fwd(self, x, y, net_, net0_, criterion, lrs, Ninflate=1.0, nd=1.0, **kw):
         rec["lrs"].append([float(v) for v in lrs])
         rec["should_sample"].append(bool(kw.get("should_sample", False)))
         rec["theta"].append(flat(runner.net.parameters()))
-        rec["mom"].append(state_mom())
+        record_state()
         cap.active, cap.draws = True, []
         try:
             return orig_forward(self, x, y, net_, net0_, criterion, lrs, Ninflate, nd, **kw)
@@ -148,7 +172,7 @@ def run_method(methods, method, cfg):
     try:
         with cap:
             loader = fake_loader(cfg["bpe"])
-            if method in ("csghmc", "csgld"):
+            if method in ("csghmc", "csgld", "adam_csghmc"):
                 for ep in range(cfg["epochs"]):
                     runner.cyclical_scheduler.current_epoch = ep
                     runner.train_one_epoch(loader)
@@ -177,9 +201,13 @@ def run_method(methods, method, cfg):
         noise=np.stack(rec["noise"]).astype(np.float32),
         theta=np.stack(rec["theta"] + [flat(runner.net.parameters())]).astype(np.float32),
     )
-    rec["mom"].append(state_mom())
+    record_state()
     out["mom"] = np.stack(rec["mom"]).astype(np.float32)
-    if method in ("csghmc", "csgld"):
+    if adam:
+        out["adam_m"] = np.stack(rec["adam_m"]).astype(np.float32)
+        out["adam_v"] = np.stack(rec["adam_v"]).astype(np.float32)
+        out["sgd_buf"] = np.stack(rec["sgd_buf"]).astype(np.float32)
+    if method in ("csghmc", "csgld", "adam_csghmc"):
         cycles = sorted(runner.cycle_theta_mom1.keys())
         out["cycles"] = np.array(cycles, np.int64)
         out["cycle_mom1"] = np.stack([runner.cycle_theta_mom1[c].numpy() for c in cycles]) \
@@ -198,6 +226,7 @@ def run_method(methods, method, cfg):
 
 
 CLIP_MAX_NORM = 40.0
+ADAM_CLIP_MAX_NORM = 4.4
 
 CONFIGS = {
     # cSGHMC (config 2 hyper-parameters, scaled to make every term visible)
@@ -237,6 +266,44 @@ CONFIGS = {
                                       hparams=dict(prior_sig=0.5, bias="uninformative",
                                                    Ninflate=10.0, nd=0.1, burnin=1, thin=3,
                                                    nst=0))),
+    # Adam-preconditioned SGHMC (methods/adam_sghmc.py): SGD with args.momentum
+    "adam_sghmc_inf": ("adam_sghmc", dict(epochs=3, bpe=5, lr=0.05, lr_head=0.1, momentum=0.5,
+                                          ND=50, torch_seed=14, init_seed=19, init_scale=0.5,
+                                          grad_seed=109, grad_scale=0.5, prior_seed=25,
+                                          hparams=dict(prior_sig=0.8, bias="informative",
+                                                       momentum_decay=0.18, Ninflate=1.0,
+                                                       nd=1.0, burnin=1, thin=2, nst=2,
+                                                       beta1=0.9, beta2=0.99, epsilon=1e-8))),
+    "adam_sghmc_uninf_nomom": ("adam_sghmc", dict(epochs=3, bpe=4, lr=0.02, lr_head=0.04,
+                                                  momentum=0.0, ND=30, torch_seed=15,
+                                                  init_seed=20, init_scale=0.5, grad_seed=110,
+                                                  grad_scale=0.5, prior_seed=26,
+                                                  hparams=dict(prior_sig=1.5,
+                                                               bias="uninformative",
+                                                               momentum_decay=0.3, Ninflate=5.0,
+                                                               nd=0.2, burnin=1, thin=1, nst=0,
+                                                               beta1=0.8, beta2=0.95,
+                                                               epsilon=1e-6))),
+    # cyclical Adam-SGHMC (methods/adam_csghmc.py): p.grad = v_mom, g / temperature,
+    # v_mom / m / v zeroed and t reset at the end of every cycle
+    "adam_csghmc_k20": ("adam_csghmc", dict(epochs=4, bpe=5, num_cycles=2, beta=0.5, lr=0.05,
+                                            lr_head=0.1, ND=50, torch_seed=16, init_seed=21,
+                                            init_scale=0.5, grad_seed=111, grad_scale=0.5,
+                                            prior_seed=27,
+                                            hparams=dict(prior_sig=0.7, bias="informative",
+                                                         momentum_decay=0.18, Ninflate=1.0,
+                                                         nd=1.0, nst=2, thin=1, burnin=0,
+                                                         beta1=0.9, beta2=0.99, epsilon=1e-8,
+                                                         temperature=0.5))),
+    "adam_csghmc_clip": ("adam_csghmc", dict(epochs=4, bpe=5, num_cycles=2, beta=0.5, lr=0.05,
+                                             lr_head=0.1, ND=50, torch_seed=17, init_seed=22,
+                                             init_scale=0.5, grad_seed=112, grad_scale=0.5,
+                                             prior_seed=28, clip_grad=ADAM_CLIP_MAX_NORM,
+                                             hparams=dict(prior_sig=0.7, bias="uninformative",
+                                                          momentum_decay=0.18, Ninflate=2.0,
+                                                          nd=0.5, nst=2, thin=1, burnin=0,
+                                                          beta1=0.9, beta2=0.999,
+                                                          epsilon=1e-8))),
     "sghmc_inf": ("sghmc", dict(epochs=3, bpe=5, lr=0.05, lr_head=0.1, ND=50, torch_seed=12,
                                 init_seed=16, init_scale=0.5, grad_seed=106, grad_scale=0.5,
                                 prior_seed=23,

@@ -28,11 +28,14 @@ def make_args(fx, tmp, device, **over):
 
 
 def replay(fx, device="cuda", noise_mode="external", div_mode="true", runner_hook=None):
+    import bayesdll_amd.adam_csghmc as adam_csghmc
+    import bayesdll_amd.adam_sghmc as adam_sghmc
     import bayesdll_amd.csghmc as csghmc
     import bayesdll_amd.csgld as csgld
     import bayesdll_amd.sghmc as sghmc
     import bayesdll_amd.sgld as sgld
-    mods = dict(csghmc=csghmc, csgld=csgld, sgld=sgld, sghmc=sghmc)
+    mods = dict(csghmc=csghmc, csgld=csgld, sgld=sgld, sghmc=sghmc, adam_sghmc=adam_sghmc,
+                adam_csghmc=adam_csghmc)
     cfg = fx["config"]
     method = cfg["method"]
     net = FakeNet(grad_seed=cfg["grad_seed"], grad_scale=cfg["grad_scale"],
@@ -50,18 +53,27 @@ def replay(fx, device="cuda", noise_mode="external", div_mode="true", runner_hoo
     if runner_hook:
         runner_hook(runner)
 
-    rec = dict(theta=[], mom=[])
+    adam = method.startswith("adam_")
+    rec = dict(theta=[], mom=[], adam_m=[], adam_v=[], sgd_buf=[])
     orig = type(model).forward
 
-    def fwd(self, *a, **k):
-        st = self.state_for(runner.net, getattr(runner, "net0", None))
+    def record(st):
         rec["theta"].append(st.theta.detach().cpu().numpy().copy())
         rec["mom"].append(st.mom.detach().cpu().numpy().copy())
+        if adam:
+            m, v = model.adam_buffers(st)
+            rec["adam_m"].append(m.cpu().numpy().copy())
+            rec["adam_v"].append(v.cpu().numpy().copy())
+            b = model.sgd_buffer
+            rec["sgd_buf"].append(np.zeros(st.n, np.float32) if b is None else b.cpu().numpy())
+
+    def fwd(self, *a, **k):
+        record(self.state_for(runner.net, getattr(runner, "net0", None)))
         return orig(self, *a, **k)
 
     model.forward = fwd.__get__(model)
     loader = fake_loader(cfg["bpe"], device=device)
-    if method in ("csghmc", "csgld"):
+    if method in ("csghmc", "csgld", "adam_csghmc"):
         for ep in range(cfg["epochs"]):
             runner.cyclical_scheduler.current_epoch = ep
             runner.train_one_epoch(loader)
@@ -72,11 +84,9 @@ def replay(fx, device="cuda", noise_mode="external", div_mode="true", runner_hoo
                 runner.seed_moments()
             _, _, bi = runner.train_one_epoch(loader, collect=(ep >= runner.burnin), bi=bi)
     torch.cuda.synchronize()
-    st = model.flat
-    rec["theta"].append(st.theta.cpu().numpy().copy())
-    rec["mom"].append(st.mom.cpu().numpy().copy())
-    out = {k: np.stack(v) for k, v in rec.items()}
-    if method in ("csghmc", "csgld"):
+    record(model.flat)
+    out = {k: np.stack(v) for k, v in rec.items() if v}
+    if method in ("csghmc", "csgld", "adam_csghmc"):
         cycles = sorted(runner.cycle_theta_mom1.keys())
         out["cycles"] = np.array(cycles, np.int64)
         out["cycle_mom1"] = np.stack([runner.cycle_theta_mom1[c].cpu().numpy() for c in cycles])

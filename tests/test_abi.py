@@ -22,7 +22,7 @@ def test_header_declares_expected_api():
     assert declared_functions() == sorted([
         "bdl_version", "bdl_last_error", "bdl_build_runs", "bdl_sgmcmc_step",
         "bdl_moments_update", "bdl_posterior_sample", "bdl_philox_normal",
-        "bdl_set_launch_config", "bdl_clip_workspace_bytes", "bdl_sgld_step_clipped"])
+        "bdl_set_launch_config", "bdl_clip_workspace_bytes", "bdl_sgld_step_clipped", "bdl_adam_step"])
 
 
 def test_library_loads_and_exports_every_declared_symbol():
@@ -44,6 +44,9 @@ int main(void) {
   printf("bdl_segment %zu\nbdl_run %zu\nbdl_step_args %zu\nbdl_moments_args %zu\nbdl_sample_args %zu\n",
          sizeof(bdl_segment), sizeof(bdl_run), sizeof(bdl_step_args), sizeof(bdl_moments_args),
          sizeof(bdl_sample_args));
+  printf("bdl_adam_args %zu\n", sizeof(bdl_adam_args));
+  P(bdl_adam_args, sgd_buf) P(bdl_adam_args, beta1) P(bdl_adam_args, bias_corr2)
+  P(bdl_adam_args, temperature) P(bdl_adam_args, grad_is_mom)
   P(bdl_step_args, runs) P(bdl_step_args, nruns) P(bdl_step_args, n) P(bdl_step_args, lr)
   P(bdl_step_args, noise_scale) P(bdl_step_args, mu) P(bdl_step_args, collect_b)
   P(bdl_step_args, seed) P(bdl_step_args, step) P(bdl_moments_args, collect_a)
@@ -68,11 +71,13 @@ def test_ctypes_layout_matches_c_header():
     assert lay["bdl_step_args"] == C.sizeof(L.StepArgs)
     assert lay["bdl_moments_args"] == C.sizeof(L.MomentsArgs)
     assert lay["bdl_sample_args"] == C.sizeof(L.SampleArgs)
+    assert lay["bdl_adam_args"] == C.sizeof(L.AdamArgs)
     for key, v in lay.items():
         if "." not in key:
             continue
         struct, field = key.split(".")
         cls = {"bdl_step_args": L.StepArgs, "bdl_moments_args": L.MomentsArgs,
+               "bdl_adam_args": L.AdamArgs,
                "bdl_sample_args": L.SampleArgs, "bdl_run": L.Run, "bdl_segment": L.Segment}[struct]
         assert getattr(cls, field).offset == v, key
 

@@ -417,3 +417,131 @@ def test_clipped_sgld_rejects_bad_arguments():
     with pytest.raises(RuntimeError, match="GRAD_READY"):
         K.sgld_step_clipped(st, 1.0, lrs=(1e-3, 1e-3), noise_scale=(0.1, 0.1),
                             noise_mode=L.NOISE_BUFFER, grad_ready=True)
+
+
+# ----------------------------------------------- Adam-preconditioned SGHMC
+def ref_adam(st, m, v, buf, *, lrs, alpha, b1, b2, aeps, t, sigma, N, nd, temp, grad_is_mom, mu,
+             first, grad_only=False):
+    """methods/adam_sghmc.py:512-553 / adam_csghmc.py:819-860 + SGD with torch
+    ops on the device (per tensor, the reference's op order)."""
+    th, vm_all, m_all, v_all, b_all = (st.theta.clone(), st.mom.clone(), m.clone(), v.clone(),
+                                       None if buf is None else buf.clone())
+    g_all = st.grad.clone()
+    for (o, k, a) in zip(st.offsets, st.numels, st.attrs):
+        if a & 4:
+            if first and b_all is not None and mu != 0:
+                b_all[o:o + k].zero_()
+            continue
+        lr = lrs[1] if a & 1 else lrs[0]
+        p, p0, g = th[o:o + k], st.prior[o:o + k], st.grad[o:o + k]
+        gs = g / temp
+        gU = gs + (p - p0) / (sigma ** 2) / N if a & 2 else gs
+        mm = b1 * m_all[o:o + k] + (1 - b1) * gU
+        vv = b2 * v_all[o:o + k] + (1 - b2) * (gU * gU)
+        m_hat = mm / (1 - b1 ** t)
+        v_hat = vv / (1 - b2 ** t)
+        pg = m_hat / (torch.sqrt(v_hat) + aeps)
+        pt = 1.0 / (torch.sqrt(v_hat) + aeps)
+        ns = nd * torch.sqrt(2 * alpha * pt / N)
+        vm = vm_all[o:o + k] * (1 - alpha) + lr * pg + ns * st.noise[o:o + k]
+        gp = vm.clone() if grad_is_mom else g + vm.clone()
+        m_all[o:o + k] = mm
+        v_all[o:o + k] = vv
+        vm_all[o:o + k] = vm
+        if grad_only:
+            g_all[o:o + k] = gp
+            continue
+        d = gp
+        if mu != 0:
+            bb = b_all[o:o + k]
+            if first:
+                bb.copy_(gp)
+            else:
+                bb.mul_(mu).add_(gp)
+            d = bb
+        p.add_(d, alpha=-lr)
+    return th, vm_all, m_all, v_all, b_all, g_all
+
+
+def _adam_case(st, *, grad_is_mom, mu, first, t, temp=1.0, grad_only=False, nd=0.05):
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(t)
+    m = torch.randn(st.n, device=DEV, generator=gen) * 1e-3
+    v = torch.rand(st.n, device=DEV, generator=gen) * 1e-6
+    buf = torch.randn(st.n, device=DEV, generator=gen) * 1e-3 if mu != 0 else None
+    kw = dict(lrs=(1e-3, 2e-3), alpha=0.18, b1=0.9, b2=0.99, aeps=1e-8, t=t, sigma=0.8, N=500.0,
+              nd=nd, temp=temp, grad_is_mom=grad_is_mom, mu=mu, first=first)
+    th_r, vm_r, m_r, v_r, b_r, g_r = ref_adam(st, m, v, buf, grad_only=grad_only, **kw)
+    g0 = st.grad.clone()
+    K.adam_step(st, L.ADAM_SGHMC_GRAD if grad_only else L.ADAM_SGHMC, adam_m=m, adam_v=v,
+                sgd_buf=buf, beta1=kw["b1"], beta2=kw["b2"], eps=kw["aeps"], t=t,
+                momentum_decay=kw["alpha"], nd=nd, temperature=temp, grad_is_mom=grad_is_mom,
+                lrs=kw["lrs"], noise_mode=L.NOISE_BUFFER, sigma2=kw["sigma"] ** 2,
+                n_data=kw["N"], mu=mu, first_step=first, momentum=mu != 0, div_mode="recip")
+    torch.cuda.synchronize()
+    # the recip-division path rounds every op where torch's device kernels do
+    assert torch.equal(m, m_r) and torch.equal(v, v_r)
+    assert torch.equal(st.mom, vm_r)
+    if grad_only:
+        assert torch.equal(st.grad, g_r)
+    else:
+        if buf is not None:
+            assert torch.equal(buf, b_r)
+        # add_(alpha=-lr): FMA or not in torch's kernel -> allow 1 ulp
+        np.testing.assert_allclose(st.theta.cpu().numpy(), th_r.cpu().numpy(), rtol=2.5e-7,
+                                   atol=0)
+        st.theta.copy_(th_r)
+        st.grad.copy_(g0)
+    st.mom.copy_(vm_r)
+
+
+def test_adam_sghmc_full_size_vit_matches_torch():
+    """ViT-L/32 (306,535,400 params): adam_sghmc (g + v_mom, SGD momentum) and
+    adam_csghmc (v_mom, temperature, SGD momentum 0) rules, first and later steps."""
+    from bayesdll_amd.shapes import vit_l_32
+    segs, readout = vit_l_32()
+    st = _state(segs, readout, bias="uninformative", need_prior=True, need_noise=True, seed=7)
+    _adam_case(st, grad_is_mom=False, mu=0.5, first=True, t=1)
+    _adam_case(st, grad_is_mom=False, mu=0.5, first=False, t=7)
+    _adam_case(st, grad_is_mom=True, mu=0.0, first=False, t=3, temp=0.5)
+
+
+@pytest.mark.parametrize("n", [1, 5, 17, 4097, 65537])
+def test_adam_sghmc_edge_sizes_frozen_and_grad_only(n):
+    rng = np.random.default_rng(n + 11)
+    cuts = sorted(set(rng.integers(1, n, size=min(7, max(n - 1, 0))).tolist())) if n > 1 else []
+    bounds = [0] + cuts + [n]
+    segs = []
+    for i in range(len(bounds) - 1):
+        name = ("fc." if i == len(bounds) - 2 else f"l{i}.") + ("bias" if i % 2 else "weight")
+        segs.append((name, (bounds[i + 1] - bounds[i],)))
+    st = _state(segs, "fc", bias="uninformative", need_noise=True, need_prior=True, seed=n)
+    if len(segs) > 2:
+        _freeze(st, {1})
+    _adam_case(st, grad_is_mom=False, mu=0.9, first=True, t=1)
+    _adam_case(st, grad_is_mom=True, mu=0.0, first=False, t=2, temp=2.0)
+    _adam_case(st, grad_is_mom=False, mu=0.0, first=False, t=4, grad_only=True)
+
+
+def test_adam_step_philox_equals_buffer():
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    segs = [("l0.weight", (300, 301)), ("l0.bias", (301,)), ("fc.weight", (10, 301)),
+            ("fc.bias", (10,))]
+    outs = []
+    for mode in ("philox", "buffer"):
+        st = _state(segs, "fc", need_noise=True, need_prior=True, seed=11)
+        m = torch.zeros(st.n, device=DEV)
+        v = torch.zeros(st.n, device=DEV)
+        if mode == "buffer":
+            st.noise.copy_(K.philox_normal(st.n, 99, 1, 5))
+        K.adam_step(st, L.ADAM_SGHMC, adam_m=m, adam_v=v, beta1=0.9, beta2=0.999, eps=1e-8, t=1,
+                    momentum_decay=0.1, nd=1.0, lrs=(1e-3, 1e-2),
+                    noise_mode=L.NOISE_PHILOX if mode == "philox" else L.NOISE_BUFFER,
+                    sigma2=1.0, n_data=100.0, seed=99, chain=1, step=5)
+        torch.cuda.synchronize()
+        outs.append((st.theta.clone(), st.mom.clone(), m, v))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

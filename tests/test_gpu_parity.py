@@ -40,16 +40,21 @@ def test_runner_replay_matches_reference(name):
     fx = load(name)
     out = replay(fx)
     assert out["theta"].shape == fx["theta"].shape
-    for key in ("theta", "mom"):
+    keys = ("theta", "mom") + tuple(k for k in ("adam_m", "adam_v", "sgd_buf") if k in fx)
+    for key in keys:
         assert rel_err(out[key], fx[key]) <= RTOL, key
         np.testing.assert_allclose(out[key], fx[key], rtol=RTOL, atol=1e-6)
     # torch-CPU division semantics + separately rounded ops: bit-exact -- except
     # with gradient clipping, whose norm is a device reduction (summation order
     # differs from torch-CPU's, so the clip coefficient may differ in the last ulp)
-    exact = fx["config"].get("clip_grad") is None
+    # ... and except the Adam samplers: torch-CPU's vectorised fp32 sqrt (Sleef,
+    # 0.5001 ulp; ISA-dependent) is not correctly rounded, the device's is
+    # (tools/fp_probe.py: 0.6-20 % of CPU sqrt results are 1 ulp off IEEE)
+    exact = (fx["config"].get("clip_grad") is None
+             and not fx["config"]["method"].startswith("adam_"))
     if exact:
-        np.testing.assert_array_equal(out["theta"], fx["theta"])
-        np.testing.assert_array_equal(out["mom"], fx["mom"])
+        for key in keys:
+            np.testing.assert_array_equal(out[key], fx[key], err_msg=key)
     if "cycles" in fx and not exact:
         np.testing.assert_array_equal(out["cycles"], fx["cycles"])
         np.testing.assert_array_equal(out["samples_per_cycle"], fx["samples_per_cycle"])
@@ -64,8 +69,11 @@ def test_runner_replay_matches_reference(name):
         np.testing.assert_array_equal(out["cycle_mom2"], fx["cycle_mom2"])
     else:
         assert out["post_cnt"] == int(fx["post_cnt"])
-        np.testing.assert_array_equal(out["post_mom1"], fx["post_mom1"])
-        np.testing.assert_array_equal(out["post_mom2"], fx["post_mom2"])
+        for key in ("post_mom1", "post_mom2"):
+            if exact:
+                np.testing.assert_array_equal(out[key], fx[key], err_msg=key)
+            elif fx[key].size:
+                assert rel_err(out[key], fx[key]) <= RTOL, key
 
 
 @pytest.mark.parametrize("name", ["csghmc_k20", "sgld_inf", "sghmc_uninf"])

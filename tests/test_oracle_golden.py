@@ -19,6 +19,11 @@ def test_oracle_matches_reference_bitexact(name):
     np.testing.assert_array_equal(out["lrs"], fx["lrs"])
     np.testing.assert_array_equal(out["theta"], fx["theta"])
     np.testing.assert_array_equal(out["mom"], fx["mom"])
+    for key in ("adam_m", "adam_v", "sgd_buf"):
+        if key in fx and key in out:
+            np.testing.assert_array_equal(out[key], fx[key], err_msg=key)
+    if fx["config"]["method"].startswith("adam_"):
+        assert "adam_m" in out and "adam_v" in out
     if fx["config"]["method"] == "csghmc":
         np.testing.assert_array_equal(out["should_sample"], fx["should_sample"])
     if "cycles" in fx:
