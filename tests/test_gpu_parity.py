@@ -180,3 +180,36 @@ def test_same_seed_matches_reference_update_on_gpu(method, bias):
     got = _product_gpu_chain(method, 6, 77, 4242, cfg, div_mode="recip")
     assert rel_err(got, ref) <= RTOL
     np.testing.assert_allclose(got, ref, rtol=RTOL, atol=1e-6)
+
+
+def test_adam_checkpoint_keys_and_roundtrip():
+    """methods/adam_sghmc.py:379-418: ckpt.pt carries SGLD's keys plus
+    momentum_buffer / m / v / t; load_ckpt restores them into the flat buffers."""
+    import os
+    from product_replay import replay
+    from bayesdll_amd._runner import load_checkpoint
+    fx = load("adam_sghmc_inf")
+    out = replay(fx, div_mode="recip")
+    runner = out["runner"]
+    model = runner.model
+    path = runner.save_ckpt(2)
+    ck = load_checkpoint(path, "cpu")
+    assert set(ck) == {"last_theta", "post_theta_mom1", "post_theta_mom2", "post_theta_cnt",
+                       "prior_sig", "optimizer", "momentum_buffer", "m", "v", "t", "epoch"}
+    assert ck["t"] == model.t == fx["theta"].shape[0] - 1
+    names = [nm for nm, _ in runner.net.named_parameters()]
+    assert list(ck["m"]) == names and list(ck["momentum_buffer"]) == names
+    m_flat = torch.cat([ck["m"][k].reshape(-1) for k in names])
+    assert torch.equal(m_flat, model.adam_buffers(model.flat)[0].cpu())
+    snap = {k: v.clone() for k, v in zip(("vm", "m", "v", "buf"),
+                                         (model.flat.mom, *model.adam_buffers(model.flat),
+                                          model.sgd_buffer))}
+    for tns in (model.flat.mom, *model.adam_buffers(model.flat), model.sgd_buffer):
+        tns.zero_()
+    model.t = 0
+    assert runner.load_ckpt(path) == 2
+    assert model.t == ck["t"]
+    for k, tns in zip(("vm", "m", "v", "buf"), (model.flat.mom, *model.adam_buffers(model.flat),
+                                               model.sgd_buffer)):
+        assert torch.equal(tns, snap[k]), k
+    assert os.path.basename(path) == "ckpt.pt"

@@ -66,6 +66,8 @@ def rel(a, b):
 
 
 def run_product(name):
+    import bayesdll_amd.adam_csghmc as adam_csghmc
+    import bayesdll_amd.adam_sghmc as adam_sghmc
     import bayesdll_amd.csghmc as csghmc
     import bayesdll_amd.sgld as sgld
     fx = load_mlp(name)
@@ -147,12 +149,14 @@ def test_mlp_sgld_config1_train_and_evaluate():
     assert abs(evals[-1][0] - fx["eval_loss"]) / fx["eval_loss"] < 1e-4
 
 
-@pytest.mark.parametrize("method", ["csghmc", "sgld", "sghmc"])
+@pytest.mark.parametrize("method", ["csghmc", "sgld", "sghmc", "adam_sghmc", "adam_csghmc"])
 def test_mlp_real_autograd_matches_reference_update_same_gpu(method):
     """Real mlp_mnist + real autograd, both sides on THIS GPU: the product's
     Model (gradients written by autograd straight into the flat buffer, fused
     update) vs the reference update (oracle's per-tensor torch ops on cuda
     tensors + torch.optim.SGD), same seed, torch noise mode."""
+    import bayesdll_amd.adam_csghmc as adam_csghmc
+    import bayesdll_amd.adam_sghmc as adam_sghmc
     import bayesdll_amd.csghmc as csghmc
     import bayesdll_amd.sghmc as sghmc
     import bayesdll_amd.sgld as sgld
@@ -164,7 +168,10 @@ def test_mlp_real_autograd_matches_reference_update_same_gpu(method):
     prior = torch.tensor(init_vector(8, n, 0.03))
     data = synthetic_mnist(9, 256, 64, device=dev)
     lrs = [1e-2, 2e-2]
-    N, nd, psig, alpha, mu = 30000.0, 0.5, 1.0, 0.18, (0.5 if method == "sgld" else 0.0)
+    N, nd, psig, alpha = 30000.0, 0.5, 1.0, 0.18
+    mu = 0.5 if method in ("sgld", "adam_sghmc") else 0.0
+    temp = 0.5 if method == "adam_csghmc" else 1.0
+    adam_kw = dict(beta1=0.9, beta2=0.99, epsilon=1e-8)
 
     def make():
         net = MLP()
@@ -183,6 +190,9 @@ def test_mlp_real_autograd_matches_reference_update_same_gpu(method):
                            {"params": [p for nm, p in net.named_parameters() if "classifier" in nm], "lr": lrs[1]}],
                           momentum=mu)
     moms = [torch.zeros_like(p) for p in net.parameters()]
+    am = [torch.zeros_like(p) for p in net.parameters()]
+    av = [torch.zeros_like(p) for p in net.parameters()]
+    t = 0
     torch.manual_seed(1234)
     for x, y in data:
         loss = crit(net(x), y)
@@ -195,7 +205,14 @@ def test_mlp_real_autograd_matches_reference_update_same_gpu(method):
                 moms = O.csghmc_update(ps, [p.grad for p in ps], moms, names, "classifier", lrs,
                                        psig, alpha, N, nd, True, eps)
                 continue
-            if method == "sghmc":
+            if method.startswith("adam_"):
+                t += 1
+                g2, moms, am, av = O.adam_sghmc_model(
+                    ps, list(net0.parameters()), [p.grad for p in ps], moms, am, av, names,
+                    "classifier", lrs, psig, "informative", alpha, adam_kw["beta1"],
+                    adam_kw["beta2"], adam_kw["epsilon"], t, N, nd, eps, temperature=temp,
+                    grad_is_mom=(method == "adam_csghmc"))
+            elif method == "sghmc":
                 g2, moms = O.sghmc_model(ps, list(net0.parameters()), [p.grad for p in ps], moms,
                                          names, "classifier", lrs, psig, "informative", alpha, N,
                                          nd, eps)
@@ -213,6 +230,11 @@ def test_mlp_real_autograd_matches_reference_update_same_gpu(method):
         model = csghmc.Model(N, prior_sig=psig, momentum_decay=alpha)
     elif method == "sghmc":
         model = sghmc.Model(N, prior_sig=psig, momentum_decay=alpha)
+    elif method == "adam_sghmc":
+        model = adam_sghmc.Model(N, prior_sig=psig, momentum_decay=alpha, **adam_kw)
+    elif method == "adam_csghmc":
+        model = adam_csghmc.Model(N, prior_sig=psig, momentum_decay=alpha, temperature=temp,
+                                  **adam_kw)
     else:
         model = sgld.Model(N, prior_sig=psig)
     model.noise_mode, model.div_mode = "torch", "recip"
