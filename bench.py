@@ -35,7 +35,9 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_ELEM = {"explore": 20, "sample": 20, "collect_init": 28, "collect": 36,
                   # sgld + SGD(momentum): theta rw, g r, theta0 r, buf (w | rw), +m1/m2 rw
-                  "sgld_first": 20, "sgld": 24, "sgld_collect": 40}
+                  "sgld_first": 20, "sgld": 24, "sgld_collect": 40,
+                  # adam_sghmc + SGD(momentum): theta, v_mom, m, v rw; g, theta0 r; buf (w | rw)
+                  "adam_first": 44, "adam": 48, "adam_collect": 64}
 
 
 def parse():
@@ -44,7 +46,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--backbone", default="vit_l_32")
-    ap.add_argument("--method", default="csghmc", choices=["csghmc", "sgld"])
+    ap.add_argument("--method", default="csghmc", choices=["csghmc", "sgld", "adam_sghmc"])
     ap.add_argument("--num-classes", type=int, default=1000)
     ap.add_argument("--thin", type=int, default=10)
     ap.add_argument("--cycles", type=int, default=4)
@@ -169,7 +171,8 @@ def main():
     else:
         launch = {"default": True, "autotuned": False}
     dev = torch.device("cuda", local)
-    sgld = a.method == "sgld"
+    adam = a.method == "adam_sghmc"
+    sgld = a.method == "sgld" or adam  # adam shares config 3's state/driver shape
     st = FlatState.from_segments(segs, readout, device=dev, need_prior=sgld)
     gen = torch.Generator(device=dev).manual_seed(42 + rank)
     if sgld:  # config 3: theta0 ~ N(0, 0.02^2) (pretrained stand-in), theta = theta0 + N(0, 1e-3^2)
@@ -217,6 +220,33 @@ def main():
             spc[0] = cnt + 1
         return kind
 
+    if adam:
+        adam_m = torch.zeros(n, dtype=torch.float32, device=dev)
+        adam_v = torch.zeros(n, dtype=torch.float32, device=dev)
+        sgd_buf = torch.empty(n, dtype=torch.float32, device=dev)
+
+    def adam_step(k, ev=None):
+        """methods/adam_sghmc.py:458-553 + SGD(momentum 0.5) (:60, :229) +
+        running moments every `thin` iterations, fused."""
+        first = k == 0
+        collect = (k + 1) % a.thin == 0
+        kind = "adam_first" if first else ("adam_collect" if collect else "adam")
+        cnt = spc[0]
+        if ev is not None:
+            ev[0].record()
+        K.adam_step(st, L.ADAM_SGHMC, adam_m=adam_m, adam_v=adam_v, sgd_buf=sgd_buf, beta1=0.9,
+                    beta2=0.999, eps=1e-8, t=k + 1, momentum_decay=alpha, nd=nd,
+                    lrs=(lr, lr_head), noise_mode=L.NOISE_PHILOX, sigma2=prior_sig ** 2,
+                    n_data=N, mu=mu, first_step=first, momentum=True,
+                    collect=L.COLLECT_MEAN if collect else L.COLLECT_NONE, mom1=m1s[0],
+                    mom2=m2s[0], collect_a=float(cnt), collect_b=float(cnt + 1),
+                    seed=42 + rank, chain=rank, step=k)
+        if ev is not None:
+            ev[1].record()
+        if collect:
+            spc[0] = cnt + 1
+        return kind
+
     def plan(k):
         cur = sched.calculate_lr(0, k, total)
         ss = sched.should_sample(0, k, total) and k % a.thin == 0
@@ -255,7 +285,7 @@ def main():
         return kind
 
     if sgld:
-        step = sgld_step  # noqa: F811
+        step = adam_step if adam else sgld_step  # noqa: F811
     for k in range(a.warmup):
         step(k)
     torch.cuda.synchronize()
@@ -318,7 +348,9 @@ def main():
         "dtype": "f32",
         "data": "synthetic (random-init theta, resident synthetic grad buffer)",
         "config": {"workload": (f"{a.backbone} cSGHMC fused leapfrog update (config 4/5)" if not sgld
-                                else f"{a.backbone} SGLD + SGD(momentum 0.5) fused update (config 3)"),
+                                else f"{a.backbone} Adam-SGHMC + SGD(momentum 0.5) fused update"
+                                if adam else
+                                f"{a.backbone} SGLD + SGD(momentum 0.5) fused update (config 3)"),
                    "params": n, "tensors": len(segs), "readout": readout,
                    "cycles": a.cycles, "thin": a.thin, "beta": 0.5, "noise": "philox",
                    "parallelism": f"{world} independent chains (1/GPU)"},

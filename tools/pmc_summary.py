@@ -7,7 +7,7 @@
   16-B/lane streaming read, so bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024;
 * profiles/pmc_traffic.json updated (read by bench.py for roofline.traffic).
 
-usage: python tools/pmc_summary.py <tag> [dest subdir, e.g. round1/kernel_v3]
+usage: python tools/pmc_summary.py <tag> [dest subdir, e.g. round1/kernel_v3] [backbone]
 """
 import csv
 import json
@@ -20,14 +20,26 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KIND = {(0, 0): "explore", (2, 0): "sample", (2, 1): "collect_init", (2, 2): "collect"}
 
 
+# bdl_step_kernel<METHOD=2 (SGLD), NOISE, COLLECT, UNROLL>
+SGLD_KIND = {(2, 0): "sgld", (2, 4): "sgld_collect"}
+# bdl_adam_kernel<NOISE, COLLECT, GRADONLY>
+ADAM_KIND = {(2, 0): "adam", (2, 4): "adam_collect"}
+FIRST_OF = {"sgld": "sgld_first", "adam": "adam_first"}  # SGD buffer created: fewer reads
+
+
 def kind_of(name):
     m = re.search(r"bdl_step_kernel<(\d+), (\d+), (\d+), (\d+)>", name)
-    if not m or int(m.group(1)) != 0:
-        return None
-    return KIND.get((int(m.group(2)), int(m.group(3))))
+    if m and int(m.group(1)) == 0:
+        return KIND.get((int(m.group(2)), int(m.group(3))))
+    if m and int(m.group(1)) == 2:
+        return SGLD_KIND.get((int(m.group(2)), int(m.group(3))))
+    m = re.search(r"bdl_adam_kernel<(\d+), (\d+), false>", name)
+    if m:
+        return ADAM_KIND.get((int(m.group(1)), int(m.group(2))))
+    return None
 
 
-def main(tag, dest=None):
+def main(tag, dest=None, backbone="vit_l_32"):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles", dest or tag)
     os.makedirs(dst, exist_ok=True)
@@ -36,7 +48,9 @@ def main(tag, dest=None):
     acc = {}
     for sub, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         rows = [r for r in csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv")))
-                if "bdl_step_kernel" in r["Kernel_Name"]]
+                if "bdl_step_kernel" in r["Kernel_Name"] or "bdl_adam_kernel" in r["Kernel_Name"]]
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        seen = set()
         with open(os.path.join(dst, f"pmc_{sub}.csv"), "w", newline="") as f:
             w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Counter_Name",
                                               "Counter_Value", "VGPR_Count", "SGPR_Count",
@@ -46,6 +60,9 @@ def main(tag, dest=None):
             for r in rows:
                 w.writerow(r)
                 k = kind_of(r["Kernel_Name"])
+                if k in FIRST_OF and k not in seen:  # the run's first step (k == 0)
+                    seen.add(k)
+                    k = FIRST_OF[k]
                 if k:
                     acc.setdefault(k, {}).setdefault(counter, []).append(float(r["Counter_Value"]))
     traffic, raw = {}, {}
@@ -53,14 +70,19 @@ def main(tag, dest=None):
         raw[k] = {c: sum(v) / len(v) for c, v in d.items()}
         if "FETCH_SIZE" in raw[k] and "WRITE_SIZE" in raw[k]:
             traffic[k] = int((2 * raw[k]["FETCH_SIZE"] + raw[k]["WRITE_SIZE"]) * 1024)
-    out = {"vit_l_32": traffic, "_source": f"profiles/{dest or tag}",
-           "_method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; bytes "
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    out.setdefault(backbone, {}).update(traffic)
+    out.setdefault("_sources", {})[backbone + ":" + ",".join(sorted(traffic))] = \
+        f"profiles/{dest or tag}"
+    out["_method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; bytes "
                       "per launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE "
-                      "reports half of a 16-B/lane streaming read, MI355X_MICROARCH.md)",
-           "_raw_kib_per_launch": raw}
-    json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
-    print(json.dumps(out, indent=1))
+                      "reports half of a 16-B/lane streaming read, MI355X_MICROARCH.md)")
+    out.setdefault("_raw_kib_per_launch", {}).setdefault(backbone, {}).update(raw)
+    json.dump(out, open(path, "w"), indent=1)
+    print(json.dumps({backbone: traffic, "raw": raw}, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None,
+         sys.argv[3] if len(sys.argv) > 3 else "vit_l_32")
