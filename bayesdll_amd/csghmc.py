@@ -105,6 +105,7 @@ class Runner:
             logger.info(f"[Epoch {ep}/{args.epochs}] Training summary: loss = "
                         f"{losses_train[ep]:.4f}, prediction error = {errors_train[ep]:.4f} "
                         f"(time: {time.time() - tic:.4f} seconds)")
+            self._epoch_end(ep, train_loader, val_loader, test_loader)
             if cycle_updated:
                 if val_loader is not None:
                     losses_val[ep], errors_val[ep], tv, lv, lav = self.evaluate(val_loader)
@@ -208,7 +209,14 @@ class Runner:
                                 f"{likelihood.mean():.6e}")
                     with torch.no_grad():
                         self.save_ckpt(epoch=sched.current_epoch)
+                    self._cycle_completed(cycle_number)
         return loss / nb_samples, error / nb_samples, cycle_updated
+
+    def _cycle_completed(self, cycle_number):
+        """Hook after a newly completed cycle was scored and checkpointed."""
+
+    def _epoch_end(self, ep, train_loader, val_loader, test_loader):
+        """Hook after each epoch's training summary (before evaluation)."""
 
     # --------------------------------------------------------------- evaluate
     def _variance_source(self, cycle):

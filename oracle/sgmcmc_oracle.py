@@ -26,9 +26,12 @@ The restated algorithm, with reference citations:
   * sgd_step          — torch.optim.SGD single-tensor path (buf = clone(grad) on
     the first step, else buf = mu*buf + grad; param.add_(buf, alpha=-lr)): the
     step the reference calls at methods/sgld.py:226, sghmc.py:229, csgld.py:253.
-  * simulate_*        — the Runner loops: csghmc.py:246-384 (Welford with the
-    doubled samples_per_cycle increment, Q2, :333-348), csgld.py:195-331,
-    sgld.py:69-107 + :193-250, sghmc.py:69-110 + :196-251.
+  * adam_sghmc_model  — methods/adam_sghmc.py:512-553 / adam_csghmc.py:819-860.
+  * clip_grad_norm    — torch.nn.utils.clip_grad_norm_ as csgld.py:250-251 calls it.
+  * simulate          — the Runner loops: csghmc.py:246-384 (Welford with the
+    doubled samples_per_cycle increment, Q2, :333-348), csghmc_fs.py (+ momentum
+    reset per completed cycle), csgld.py:195-331, adam_csghmc.py:262-413,
+    sgld.py:69-107 + :193-250, sghmc.py:69-110 + :196-251, adam_sghmc.py.
 """
 from __future__ import annotations
 
@@ -270,6 +273,9 @@ def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
         rec["adam_m"].append(_cat(am))
         rec["adam_v"].append(_cat(av))
 
+    fs = method == "csghmc_fs"  # csghmc + momentum zeroed after each completed cycle
+    if fs:
+        method = "csghmc"
     if method in ("csghmc", "csgld", "adam_csghmc"):
         sched = CyclicalSchedule(lr0, cfg.get("num_cycles", 10), epochs, cfg.get("beta", 0.5))
         alpha = float(hp.get("momentum_decay", 0.0))
@@ -347,6 +353,8 @@ def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
                     c = sched.get_cycle_number(ep, b, bpe)
                     if c > current_cycle:
                         current_cycle = c
+                        if fs:  # csghmc_fs.py:590-591 -> _reset_optimizer_states (:119-131)
+                            moms = [torch.zeros_like(p) for p in params]
         rec["theta"].append(_cat(params))
         if adam:
             adam_rec()

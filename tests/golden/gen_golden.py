@@ -51,6 +51,7 @@ def import_reference():
     import methods.adam_csghmc
     import methods.adam_sghmc
     import methods.csghmc
+    import methods.csghmc_fs
     import methods.csgld
     import methods.cyclical
     import methods.sghmc
@@ -124,7 +125,7 @@ def run_method(methods, method, cfg):
     orig_forward = model_cls.forward
 
     def state_mom():
-        if method in ("csghmc", "sghmc", "adam_sghmc", "adam_csghmc"):
+        if method in ("csghmc", "csghmc_fs", "sghmc", "adam_sghmc", "adam_csghmc"):
             if not hasattr(runner.model, "momentum_buffer"):
                 return np.zeros(n, np.float32)
             return torch.cat([runner.model.momentum_buffer[nm].reshape(-1)
@@ -172,7 +173,7 @@ def run_method(methods, method, cfg):
     try:
         with cap:
             loader = fake_loader(cfg["bpe"])
-            if method in ("csghmc", "csgld", "adam_csghmc"):
+            if method in ("csghmc", "csghmc_fs", "csgld", "adam_csghmc"):
                 for ep in range(cfg["epochs"]):
                     runner.cyclical_scheduler.current_epoch = ep
                     runner.train_one_epoch(loader)
@@ -207,7 +208,7 @@ def run_method(methods, method, cfg):
         out["adam_m"] = np.stack(rec["adam_m"]).astype(np.float32)
         out["adam_v"] = np.stack(rec["adam_v"]).astype(np.float32)
         out["sgd_buf"] = np.stack(rec["sgd_buf"]).astype(np.float32)
-    if method in ("csghmc", "csgld", "adam_csghmc"):
+    if method in ("csghmc", "csghmc_fs", "csgld", "adam_csghmc"):
         cycles = sorted(runner.cycle_theta_mom1.keys())
         out["cycles"] = np.array(cycles, np.int64)
         out["cycle_mom1"] = np.stack([runner.cycle_theta_mom1[c].numpy() for c in cycles]) \
@@ -243,6 +244,13 @@ CONFIGS = {
                                   hparams=dict(prior_sig=1.0, bias="uninformative",
                                                momentum_decay=0.3, Ninflate=2.0, nd=0.5,
                                                burnin=0, thin=1, nst=2))),
+    # csghmc_fs: csghmc + momentum zeroed after every completed cycle
+    "csghmc_fs_k20": ("csghmc_fs", dict(epochs=4, bpe=5, num_cycles=2, beta=0.5, lr=0.05,
+                                        lr_head=0.1, ND=50, torch_seed=20, init_seed=23,
+                                        init_scale=0.5, grad_seed=113, grad_scale=0.5,
+                                        hparams=dict(prior_sig=0.7, bias="informative",
+                                                     momentum_decay=0.18, Ninflate=1.0, nd=1.0,
+                                                     burnin=0, thin=2, nst=2))),
     "csgld_k20": ("csgld", dict(epochs=4, bpe=5, num_cycles=2, beta=0.5, lr=0.05, lr_head=0.1,
                                 momentum=0.5, ND=50, torch_seed=9, init_seed=13, init_scale=0.5,
                                 grad_seed=103, grad_scale=0.5,

@@ -7,7 +7,7 @@ import numpy as np
 from fakenet import grads_for_step
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-FIXTURES = ["csghmc_k20", "csghmc_k21", "csgld_k20", "csgld_clip", "sgld_inf", "sgld_uninf_nomom",
+FIXTURES = ["csghmc_k20", "csghmc_k21", "csghmc_fs_k20", "csgld_k20", "csgld_clip", "sgld_inf", "sgld_uninf_nomom",
             "sghmc_inf", "sghmc_uninf", "adam_sghmc_inf", "adam_sghmc_uninf_nomom",
             "adam_csghmc_k20", "adam_csghmc_clip"]
 

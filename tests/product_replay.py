@@ -31,10 +31,11 @@ def replay(fx, device="cuda", noise_mode="external", div_mode="true", runner_hoo
     import bayesdll_amd.adam_csghmc as adam_csghmc
     import bayesdll_amd.adam_sghmc as adam_sghmc
     import bayesdll_amd.csghmc as csghmc
+    import bayesdll_amd.csghmc_fs as csghmc_fs
     import bayesdll_amd.csgld as csgld
     import bayesdll_amd.sghmc as sghmc
     import bayesdll_amd.sgld as sgld
-    mods = dict(csghmc=csghmc, csgld=csgld, sgld=sgld, sghmc=sghmc, adam_sghmc=adam_sghmc,
+    mods = dict(csghmc=csghmc, csghmc_fs=csghmc_fs, csgld=csgld, sgld=sgld, sghmc=sghmc, adam_sghmc=adam_sghmc,
                 adam_csghmc=adam_csghmc)
     cfg = fx["config"]
     method = cfg["method"]
@@ -73,7 +74,7 @@ def replay(fx, device="cuda", noise_mode="external", div_mode="true", runner_hoo
 
     model.forward = fwd.__get__(model)
     loader = fake_loader(cfg["bpe"], device=device)
-    if method in ("csghmc", "csgld", "adam_csghmc"):
+    if method in ("csghmc", "csghmc_fs", "csgld", "adam_csghmc"):
         for ep in range(cfg["epochs"]):
             runner.cyclical_scheduler.current_epoch = ep
             runner.train_one_epoch(loader)
@@ -86,7 +87,7 @@ def replay(fx, device="cuda", noise_mode="external", div_mode="true", runner_hoo
     torch.cuda.synchronize()
     record(model.flat)
     out = {k: np.stack(v) for k, v in rec.items() if v}
-    if method in ("csghmc", "csgld", "adam_csghmc"):
+    if method in ("csghmc", "csghmc_fs", "csgld", "adam_csghmc"):
         cycles = sorted(runner.cycle_theta_mom1.keys())
         out["cycles"] = np.array(cycles, np.int64)
         out["cycle_mom1"] = np.stack([runner.cycle_theta_mom1[c].cpu().numpy() for c in cycles])

@@ -24,7 +24,7 @@ def test_oracle_matches_reference_bitexact(name):
             np.testing.assert_array_equal(out[key], fx[key], err_msg=key)
     if fx["config"]["method"].startswith("adam_"):
         assert "adam_m" in out and "adam_v" in out
-    if fx["config"]["method"] == "csghmc":
+    if fx["config"]["method"] in ("csghmc", "csghmc_fs"):
         np.testing.assert_array_equal(out["should_sample"], fx["should_sample"])
     if "cycles" in fx:
         np.testing.assert_array_equal(out["cycles"], fx["cycles"])
