@@ -66,8 +66,6 @@ def rel(a, b):
 
 
 def run_product(name):
-    import bayesdll_amd.adam_csghmc as adam_csghmc
-    import bayesdll_amd.adam_sghmc as adam_sghmc
     import bayesdll_amd.csghmc as csghmc
     import bayesdll_amd.sgld as sgld
     fx = load_mlp(name)
@@ -289,3 +287,55 @@ def test_checkpoint_format_and_roundtrip(tmp_path):
     assert sg.post_theta_cnt == ck["epoch"]  # the reference's cnt = epoch (sgld.py:394)
     sg.load_ckpt(os.path.join(sg.args.log_dir, "ckpt.pt"), exact_count=True)
     assert sg.post_theta_cnt == ck["post_theta_cnt"] and ck["post_theta_cnt"] <= cnt
+
+
+@pytest.mark.parametrize("method", ["csghmc_fs", "adam_csghmc", "adam_sghmc"])
+def test_variant_runners_train_end_to_end(method, tmp_path):
+    """Runner.train() of the variants on the real mlp_mnist backbone (Philox
+    noise): csghmc_fs saves full-sample snapshots and writes the BMA results;
+    adam_csghmc / csghmc_fs zero their momentum (and Adam state) at cycle ends
+    and re-initialise the network with perform_cold_restarts; adam_sghmc
+    checkpoints its Adam state."""
+    import importlib
+    import os
+    mod = importlib.import_module(f"bayesdll_amd.{method}")
+    dev = "cuda"
+    torch.manual_seed(0)
+    net = MLP().to(dev)
+    train = synthetic_mnist(3, 256, 64, device=dev)
+    test = synthetic_mnist(4, 128, 64, device=dev)
+    hp = dict(prior_sig=1.0, bias="informative", Ninflate=1.0, nd=0.01, burnin=1, thin=2,
+              nst=2, momentum_decay=0.18, perform_cold_restarts="true")
+    args = SimpleNamespace(device=dev, ND=1000, pretrained=None, lr=1e-2, lr_head=2e-2,
+                           momentum=0.5, epochs=4, num_cycles=2, proportion_exploration=0.5,
+                           full_sample=False, test_eval_freq=1, ece_num_bins=15,
+                           log_dir=str(tmp_path), num_classes=10,
+                           hparams={k: str(v) for k, v in hp.items()})
+    runner = mod.Runner(net, None, args, logging.getLogger("variant"))
+    resets = []
+    if method != "adam_sghmc":
+        orig = runner._cycle_completed
+
+        def spy(c):
+            orig(c)
+            resets.append((c, runner.model.flat.mom.abs().max().item()))
+        runner._cycle_completed = spy
+    res = runner.train(train, None, test)
+    torch.cuda.synchronize()
+    files = set(os.listdir(tmp_path))
+    st = runner.model.flat
+    assert torch.isfinite(st.theta).all()
+    if method == "adam_sghmc":
+        assert "ckpt.pt" in files
+        from bayesdll_amd._runner import load_checkpoint
+        ck = load_checkpoint(os.path.join(tmp_path, "ckpt.pt"), "cpu")
+        assert {"momentum_buffer", "m", "v", "t"} <= set(ck)
+        return
+    assert {"1_ckpt.pt", "2_ckpt.pt"} <= files
+    assert [c for c, _ in resets] == [1, 2] and all(m == 0.0 for _, m in resets)
+    assert np.isfinite(res["losses_test"]).all()
+    if method == "csghmc_fs":
+        assert {"full_samples_net_ep0.pth", "full_samples_net_ep2.pth",
+                "bma_evaluation_results.pkl", "logits_test_bma.pkl"} <= files
+    else:
+        assert runner.model.t == 0  # reset at the last cycle end
