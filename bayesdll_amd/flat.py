@@ -115,6 +115,21 @@ class FlatState:
         self.attrs = attrs
         self.runs = build_runs(self.offsets, self.numels, attrs, self.n).to(dev)
         self.nruns = int(self.runs.shape[0])
+        self._base_runs = (self.runs, self.nruns)
+        self._skip_tables = {}
+        # which parameters received a gradient in the current backward: the
+        # reference skips a parameter whose .grad is None after net.zero_grad()
+        # + backward (`if p.grad is not None`, e.g. methods/csghmc.py:749)
+        self._touched = [False] * len(self.params)
+        self._hooks = [p.register_post_accumulate_grad_hook(self._mark(i))
+                       for i, p in enumerate(self.params) if p.requires_grad]
+
+    def _mark(self, i):
+        touched = self._touched
+
+        def hook(_p):
+            touched[i] = True
+        return hook
 
     @classmethod
     def from_segments(cls, segments, readout_name, *, bias="informative", device="cuda",
@@ -142,6 +157,10 @@ class FlatState:
         self.attrs = segment_attrs(self.names, readout_name, bias, self.requires_grad)
         self.runs = build_runs(self.offsets, self.numels, self.attrs, self.n).to(self.device)
         self.nruns = int(self.runs.shape[0])
+        self._base_runs = (self.runs, self.nruns)
+        self._skip_tables = {}
+        self._touched = []
+        self._hooks = []
         return self
 
     # ---------------------------------------------------------------- grads
@@ -158,26 +177,57 @@ class FlatState:
     def zero_grad(self):
         """Replaces net.zero_grad(): keep .grad bound to the flat buffer."""
         self.grad.zero_()
+        for i in range(len(self._touched)):
+            self._touched[i] = False
         for p, ptr in zip(self.params, self._grad_ptrs):
             if ptr is not None and (p.grad is None or p.grad.data_ptr() != ptr):
                 self._bind_grads()
                 break
 
     def sync_grads(self):
-        """After backward: if user code replaced a .grad, copy it into the flat buffer."""
+        """After backward: if user code replaced a .grad, copy it into the flat
+        buffer; then select the run table of this step — parameters that got no
+        gradient (unused in the forward pass, or .grad set to None) are
+        skipped, exactly like the reference's `if p.grad is not None`."""
         rebind = False
-        for p, o, k, ptr in zip(self.params, self.offsets, self.numels, self._grad_ptrs):
+        untouched = []
+        for i, (p, o, k, ptr) in enumerate(zip(self.params, self.offsets, self.numels,
+                                               self._grad_ptrs)):
             if ptr is None:
                 continue
             g = p.grad
             if g is None:
                 self.grad[o:o + k].zero_()
+                untouched.append(i)
                 rebind = True
-            elif g.data_ptr() != ptr:
-                self.grad[o:o + k].copy_(g.reshape(-1))
-                rebind = True
+            else:
+                if g.data_ptr() != ptr:
+                    self.grad[o:o + k].copy_(g.reshape(-1))
+                    rebind = True
+                if self._touched and not self._touched[i]:
+                    untouched.append(i)
         if rebind:
             self._bind_grads()
+        self._select_runs(tuple(untouched))
+
+    def _select_runs(self, untouched):
+        if not untouched:
+            self.runs, self.nruns = self._base_runs
+            return
+        tab = self._skip_tables.get(untouched)
+        if tab is None:
+            attrs = list(self.attrs)
+            for i in untouched:
+                attrs[i] |= L.ATTR_SKIP
+            runs = build_runs(self.offsets, self.numels, attrs, self.n).to(self.device)
+            tab = self._skip_tables[untouched] = (runs, int(runs.shape[0]))
+        self.runs, self.nruns = tab
+
+    def has_grad(self, i):
+        """Did parameter i receive a gradient in the current step?"""
+        if not self.requires_grad[i]:
+            return False
+        return not self._touched or self._touched[i]
 
     def check_bound(self):
         """Raise if a parameter no longer aliases the flat theta buffer."""
@@ -194,8 +244,8 @@ class FlatState:
         """Per-tensor standard-normal draws in named_parameters order: the same
         generator calls as the reference's torch.randn_like(p) per tensor
         (methods/csghmc.py:766) — used by the "torch" parity noise mode."""
-        for v, rg in zip(self.views(self.noise), self.requires_grad):
-            if rg:
+        for i, v in enumerate(self.views(self.noise)):
+            if self.has_grad(i):
                 v.normal_(generator=generator)
         return self.noise
 
