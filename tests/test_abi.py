@@ -136,3 +136,52 @@ def test_step_rejects_null_and_misaligned_pointers_without_launching():
     assert rc == -2 and b"aligned" in L.lib().bdl_last_error()
     a.theta, a.method = 0x1000, 9
     assert L.lib().bdl_sgmcmc_step(a, None) == -3
+
+
+def test_entry_points_validate_before_touching_the_device():
+    """Argument errors come back as negative bdl_status codes with a message,
+    before any HIP call (so this runs without a GPU)."""
+    from bayesdll_amd import _lib as L
+    h = L.lib()
+    a = L.StepArgs()
+    assert h.bdl_sgmcmc_step(None, None) == -1                     # BDL_ERR_NULL
+    assert b"null args" in h.bdl_last_error()
+    a.n, a.method = 8, 9
+    assert h.bdl_sgmcmc_step(a, None) == -3                         # unknown method
+    a.method, a.noise_mode = L.CSGHMC, 7
+    assert h.bdl_sgmcmc_step(a, None) == -3                         # unknown noise mode
+    a.noise_mode = L.NOISE_NONE
+    assert h.bdl_sgmcmc_step(a, None) == -1                         # theta/grad/runs missing
+    a.theta, a.grad, a.mom, a.runs, a.nruns = 0x1000, 0x2000, 0x3000, 0x4000, 5000
+    assert h.bdl_sgmcmc_step(a, None) == -5                         # > 4096 runs
+    a.nruns = 1
+    a.grad = 0x2004
+    assert h.bdl_sgmcmc_step(a, None) == -2                         # misaligned vector
+    a.grad = 0x2000
+    a.method = L.SGLD
+    assert h.bdl_sgmcmc_step(a, None) == -1                         # sgld needs prior_mean
+    a.n = 0
+    assert h.bdl_sgmcmc_step(a, None) == 0                          # empty: no-op
+    # clipped step: only SGLD, max_norm > 0, no GRAD_READY
+    a.n, a.prior_mean = 8, 0x5000
+    a.method = L.CSGHMC
+    assert h.bdl_sgld_step_clipped(a, 1.0, C.c_void_p(0x6000), None) == -3
+    a.method = L.SGLD
+    assert h.bdl_sgld_step_clipped(a, 0.0, C.c_void_p(0x6000), None) == -3
+    assert h.bdl_sgld_step_clipped(a, 1.0, None, None) == -1
+    a.flags = L.FLAG_GRAD_READY
+    assert h.bdl_sgld_step_clipped(a, 1.0, C.c_void_p(0x6000), None) == -3
+    a.flags = 0
+    assert h.bdl_clip_workspace_bytes(10 ** 9) >= 8
+    # Adam: method, Adam buffers, SGD buffer with MOMENTUM
+    ad = L.AdamArgs()
+    assert h.bdl_adam_step(a, ad, None) == -3                       # method is SGLD
+    a.method = L.ADAM_SGHMC
+    assert h.bdl_adam_step(a, ad, None) == -1                       # adam_m / adam_v missing
+    ad.adam_m, ad.adam_v = 0x7000, 0x8000
+    a.flags = L.FLAG_MOMENTUM
+    assert h.bdl_adam_step(a, ad, None) == -1                       # sgd_buf missing
+    a.flags, a.collect = 0, L.COLLECT_WELFORD
+    a.mom1 = 0x9000
+    assert h.bdl_adam_step(a, ad, None) == -3                       # Welford not an Adam collect
+    assert b"bdl_adam_step" in h.bdl_last_error()
