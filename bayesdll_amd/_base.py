@@ -49,6 +49,7 @@ class FusedModelBase(nn.Module):
 
     need_prior = False
     need_mom = True
+    tune_method = "sgld"  # which production kernel autotune_once times for this sampler
 
     def __init__(self):
         super().__init__()
@@ -71,6 +72,10 @@ class FusedModelBase(nn.Module):
                                     need_prior=self.need_prior, need_mom=self.need_mom,
                                     need_noise=self.noise_mode != "philox")
             self._state_net = net
+            # launch geometry for this device and size (speed only: results
+            # never depend on it)
+            from . import kernels as K
+            K.autotune_once(self._state.n, self._state.device, self.tune_method)
         return self._state
 
     @property

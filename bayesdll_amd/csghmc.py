@@ -295,6 +295,7 @@ class Model(FusedModelBase):
 
     need_prior = False  # Q1: theta0 never enters the csghmc update
     need_mom = True
+    tune_method = "csghmc"
 
     def __init__(self, ND, runner=None, prior_sig=1.0, bias="informative", momentum_decay=0.05):
         super().__init__()

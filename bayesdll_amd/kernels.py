@@ -185,41 +185,86 @@ def set_launch_config(blocks_per_cu=0, unroll=0, grid_stride=0):
 
 # Launch geometries worth trying on gfx950 (workgroups/CU, float4 groups in
 # flight per lane, grid-stride): the sweep (profiles/round1/kernel_v1) shows the optimum
-# moving between these from one device to the next.
+# moving between these from one device to the next.  Only the cSGHMC kernel
+# has unroll variants; the others are tuned over workgroups/CU.
 AUTOTUNE_CANDIDATES = ((2, 1, 1), (1, 4, 1), (3, 1, 1), (2, 4, 1), (1, 2, 1))
+AUTOTUNE_CANDIDATES_2 = ((1, 2, 1), (2, 2, 1), (3, 2, 1), (4, 2, 1))
+_TUNED = {}
 
 
-def autotune(n, device=None, reps=6, candidates=AUTOTUNE_CANDIDATES):
+def autotune(n, device=None, reps=6, candidates=None, method="csghmc"):
     """Pick the fastest launch geometry for an n-element sweep on this device.
 
     The update of every element is independent of the launch geometry (noise
     is keyed by element index), so the choice changes speed only, never
-    results.  Times the cSGHMC exploration kernel on scratch buffers (3 x n
-    fp32, freed afterwards) and installs the winner process-wide.  Returns
+    results.  Times the method's production kernel (cSGHMC exploration; SGLD
+    + SGD momentum with Philox noise; Adam-SGHMC + SGD momentum) on scratch
+    buffers (freed afterwards) and installs the winner process-wide.  Returns
     (config, {config: ms})."""
     import numpy as np
 
     from .flat import FlatState
     dev = torch.device(device) if device is not None else torch.device("cuda",
                                                                         torch.cuda.current_device())
-    st = FlatState.from_segments([("w", (int(n),))], None, device=dev)
+    if candidates is None:
+        candidates = AUTOTUNE_CANDIDATES if method == "csghmc" else AUTOTUNE_CANDIDATES_2
+    st = FlatState.from_segments([("w", (int(n),))], None, device=dev,
+                                 need_prior=method != "csghmc")
     st.theta.zero_()
-    kw = dict(lrs=(1e-4, 1e-4), noise_scale=(0.0, 0.0), noise_mode=L.NOISE_NONE,
-              one_minus_alpha=0.9, prior_sig=1.0)
+    if method == "csghmc":
+        kw = dict(lrs=(1e-4, 1e-4), noise_scale=(0.0, 0.0), noise_mode=L.NOISE_NONE,
+                  one_minus_alpha=0.9, prior_sig=1.0)
+
+        def launch():
+            sgmcmc_step(st, L.CSGHMC, **kw)
+    elif method == "sgld":
+        st.prior.zero_()
+        kw = dict(lrs=(1e-4, 1e-4), noise_scale=(1e-3, 1e-3), noise_mode=L.NOISE_PHILOX,
+                  sigma2=1.0, n_data=1e6, mu=0.5, momentum=True)
+
+        def launch():
+            sgmcmc_step(st, L.SGLD, **kw)
+    elif method == "adam":
+        st.prior.zero_()
+        m = torch.zeros_like(st.theta)
+        v = torch.zeros_like(st.theta)
+        buf = torch.zeros_like(st.theta)
+        kw = dict(adam_m=m, adam_v=v, sgd_buf=buf, beta1=0.9, beta2=0.999, eps=1e-8, t=3,
+                  momentum_decay=0.1, nd=0.01, lrs=(1e-4, 1e-4), noise_mode=L.NOISE_PHILOX,
+                  sigma2=1.0, n_data=1e6, mu=0.5, momentum=True)
+
+        def launch():
+            adam_step(st, L.ADAM_SGHMC, **kw)
+    else:
+        raise ValueError(f"autotune: unknown method {method!r}")
     times = {}
     for cfg in candidates:
         set_launch_config(*cfg)
         for _ in range(2):
-            sgmcmc_step(st, L.CSGHMC, **kw)
+            launch()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(reps)]
         for e0, e1 in ev:
             e0.record()
-            sgmcmc_step(st, L.CSGHMC, **kw)
+            launch()
             e1.record()
         torch.cuda.synchronize(dev)
         times[cfg] = float(np.median([a.elapsed_time(b) for a, b in ev]))
     best = min(times, key=times.get)
     set_launch_config(*best)
     del st
+    torch.cuda.empty_cache()
     return best, times
+
+
+def autotune_once(n, device, method):
+    """autotune() once per (n, device, method) in this process; later calls
+    only re-install the cached winner.  BDL_AUTOTUNE=0 keeps the defaults."""
+    if os.environ.get("BDL_AUTOTUNE", "1") == "0":
+        return None
+    key = (int(n), str(device), method)
+    if key not in _TUNED:
+        _TUNED[key] = autotune(n, device, method=method)[0]
+    else:
+        set_launch_config(*_TUNED[key])
+    return _TUNED[key]

@@ -164,10 +164,13 @@ def main():
     elif not a.no_autotune:
         # untimed setup (like cudnn.benchmark): pick the launch geometry for
         # this device; results are identical under every geometry
-        best, tuned = K.autotune(sum(int(np.prod(s)) for _, s in segs), device=local)
+        best, tuned = K.autotune(sum(int(np.prod(s)) for _, s in segs), device=local,
+                                 method={"csghmc": "csghmc", "sgld": "sgld",
+                                         "adam_sghmc": "adam"}[a.method])
         launch = {"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
                   "autotuned": True,
-                  "candidates_ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4) for c, t in tuned.items()}}
+                  "candidates_ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4) for c, t in tuned.items()},
+                  "tuned_on": a.method}
     else:
         launch = {"default": True, "autotuned": False}
     dev = torch.device("cuda", local)
@@ -308,6 +311,27 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     assert torch.isfinite(st.theta[:1 << 20]).all()
+    collective = None
+    if dist is not None:
+        # informational, after the timed region: the one cross-chain exchange
+        # (posterior-predictive average of a [128, 1000] fp32 batch, bayesdll_amd.chains)
+        from bayesdll_amd import chains
+        logp = torch.log_softmax(torch.randn(128, 1000, device=dev if dist.get_backend() != "gloo"
+                                             else "cpu"), dim=1)
+        for _ in range(3):
+            chains.average_predictive(logp)
+        if logp.is_cuda:
+            torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(20):
+            out_lp = chains.average_predictive(logp)
+        if logp.is_cuda:
+            torch.cuda.synchronize()
+        collective = {"op": "all_reduce(SUM) of [128, 1000] fp32 predictive (chains.average_predictive)",
+                      "backend": dist.get_backend(),
+                      "ms": round((time.perf_counter() - t1) / 20 * 1e3, 4),
+                      "finite": bool(torch.isfinite(out_lp).all())}
 
     per = {}
     for kind, (e0, e1) in zip(kinds, events):
@@ -355,6 +379,7 @@ def main():
                    "cycles": a.cycles, "thin": a.thin, "beta": 0.5, "noise": "philox",
                    "parallelism": f"{world} independent chains (1/GPU)"},
         "hbm_gbs": round(hbm_gbs * world, 1),
+        "eval_collective": collective,
         "launch": launch,
         "kernels": table,
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
