@@ -193,6 +193,26 @@ class Runner:
         ratio = cnt / (cnt - 1) if cnt > 1 else 1.0
         return self.post_theta_mom2, L.VAR_RAW_MOMENTS, ratio
 
+    def get_mean_vars_from_moments(self):
+        """methods/sgld.py:324-350: net-shaped posterior mean and (if nst > 0)
+        variance ratio*(m2 - m1^2) clamped at 1e-12.  The fused evaluation
+        path (`evaluate`) never materialises these; this is the reference's
+        public helper, computed with the same torch ops on the device."""
+        with torch.no_grad():
+            post_theta_mean = copy.deepcopy(self.net)
+            torch.nn.utils.vector_to_parameters(self.post_theta_mom1,
+                                                post_theta_mean.parameters())
+        post_theta_vars = None
+        if self.nst > 0:
+            cnt = self.post_theta_cnt
+            ratio = cnt / (cnt - 1) if cnt > 1 else 1.0
+            with torch.no_grad():
+                vec = ratio * (self.post_theta_mom2 - self.post_theta_mom1 ** 2)
+                vec.clamp_(min=1e-12)
+                post_theta_vars = copy.deepcopy(self.net)
+                torch.nn.utils.vector_to_parameters(vec, post_theta_vars.parameters())
+        return post_theta_mean, post_theta_vars
+
     def evaluate(self, test_loader):
         m2, mode, ratio = self.get_var_source() if self.nst > 0 else (None, L.VAR_GIVEN, 1.0)
         return R.sample_average_evaluate(self, test_loader, self.post_theta_mom1, m2, mode, ratio)

@@ -213,3 +213,19 @@ def test_adam_checkpoint_keys_and_roundtrip():
                                                model.sgd_buffer)):
         assert torch.equal(tns, snap[k]), k
     assert os.path.basename(path) == "ckpt.pt"
+
+
+def test_get_mean_vars_from_moments_matches_reference_formula():
+    """methods/sgld.py:324-350 on the replayed sgld chain."""
+    from product_replay import replay
+    fx = load("sgld_inf")
+    runner = replay(fx)["runner"]
+    mean_net, var_net = runner.get_mean_vars_from_moments()
+    m1 = torch.from_numpy(fx["post_mom1"])
+    m2 = torch.from_numpy(fx["post_mom2"])
+    cnt = int(fx["post_cnt"])
+    want = (cnt / (cnt - 1) * (m2 - m1 ** 2)).clamp_(min=1e-12)
+    got_mean = torch.nn.utils.parameters_to_vector(mean_net.parameters()).cpu()
+    got_var = torch.nn.utils.parameters_to_vector(var_net.parameters()).cpu()
+    assert torch.equal(got_mean, m1)
+    assert torch.allclose(got_var, want, rtol=1e-6, atol=1e-12)
