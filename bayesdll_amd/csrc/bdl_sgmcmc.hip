@@ -590,10 +590,9 @@ __device__ __forceinline__ void adam_core(const KArgs& a, const AdamConst& c, fl
   }
 }
 
-template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, bool PRIOR>
+template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, bool PRIOR, int U>
 __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, int64_t gb,
                                           float eta) {
-  constexpr int U = 2;
   constexpr bool kReadMoments = (COLLECT == BDL_COLLECT_MEAN);
   const f4v z = {0.f, 0.f, 0.f, 0.f};
   f4v th[U], g[U], vm[U], m[U], v[U], buf[U], t0[U], ep[U], m1[U], m2[U];
@@ -653,7 +652,7 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
   }
 }
 
-template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY>
+template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, int U>
 __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, int64_t gb,
                                           int64_t gend) {
   const int64_t n = a.n;
@@ -661,7 +660,7 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
   StepConst cc;
   cc.inv_ca = c.inv_ca;
   cc.inv_cb = c.inv_cb;
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
     if (gi >= gend) continue;
     const int64_t e = gi * 4;
@@ -712,7 +711,7 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
   }
 }
 
-template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY>
+template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, int U>
 __device__ __forceinline__ void adam_body(const KArgs& a) {
   AdamConst c;
   c.sgd_mom = !GRADONLY && (a.flags & BDL_FLAG_MOMENTUM);
@@ -726,7 +725,7 @@ __device__ __forceinline__ void adam_body(const KArgs& a) {
   c.inv_bc2 = a.inv_bc2;
   c.inv_ca = a.inv_ca;
   c.inv_cb = a.inv_cb;
-  constexpr int64_t kIter = (int64_t)kBlock * 2;
+  constexpr int64_t kIter = (int64_t)kBlock * U;
   const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
   for (int i = threadIdx.x; i < a.nruns; i += kBlock) s_runs[i] = a.runs[i];
   __syncthreads();
@@ -738,21 +737,21 @@ __device__ __forceinline__ void adam_body(const KArgs& a) {
     if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 && !(attr & BDL_ATTR_SKIP)) {
       const float eta = (attr & BDL_ATTR_HEAD) ? a.lr1 : a.lr0;
       if (attr & BDL_ATTR_PRIOR)
-        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, true>(a, c, gb, eta);
+        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, true, U>(a, c, gb, eta);
       else
-        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, false>(a, c, gb, eta);
+        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, false, U>(a, c, gb, eta);
     } else {
-      adam_slow<NOISE, COLLECT, RECIP, GRADONLY>(a, c, gb, gend);
+      adam_slow<NOISE, COLLECT, RECIP, GRADONLY, U>(a, c, gb, gend);
     }
   }
 }
 
-template <int NOISE, int COLLECT, bool GRADONLY>
+template <int NOISE, int COLLECT, bool GRADONLY, int U>
 __global__ __launch_bounds__(kBlock) void bdl_adam_kernel(const KArgs a) {
   if (a.flags & BDL_FLAG_RECIP_DIV)
-    adam_body<NOISE, COLLECT, true, GRADONLY>(a);
+    adam_body<NOISE, COLLECT, true, GRADONLY, U>(a);
   else
-    adam_body<NOISE, COLLECT, false, GRADONLY>(a);
+    adam_body<NOISE, COLLECT, false, GRADONLY, U>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -1014,9 +1013,13 @@ using StepKernel = void (*)(const KArgs);
 
 template <int METHOD, int NOISE, int COLLECT>
 StepKernel pick_unroll(int unroll) {
-  // Only the cSGHMC (headline) kernel is instantiated at every unroll depth;
-  // the other methods use the default depth to keep build time down.
-  if constexpr (METHOD != BDL_CSGHMC) {
+  // Every unroll depth for cSGHMC and for the noise-bearing SGHMC / SGLD
+  // production kernels; the *_GRAD and test-only noise-free variants use the
+  // default depth to keep build time down.
+  constexpr bool kAllDepths =
+      METHOD == BDL_CSGHMC ||
+      ((METHOD == BDL_SGLD || METHOD == BDL_SGHMC) && NOISE != BDL_NOISE_NONE);
+  if constexpr (!kAllDepths) {
     (void)unroll;
     return bdl_step_kernel<METHOD, NOISE, COLLECT, 2>;
   } else {
@@ -1079,28 +1082,48 @@ StepKernel pick_step(int method, int noise, int collect, int unroll) {
   return nullptr;
 }
 
+template <int NOISE, int COLLECT>
+StepKernel pick_adam_unroll(int unroll) {
+  // unroll variants only where production runs (noise on); the test-only
+  // NONE mode keeps the default depth
+  if constexpr (NOISE == BDL_NOISE_NONE) {
+    (void)unroll;
+    return bdl_adam_kernel<NOISE, COLLECT, false, 2>;
+  } else {
+    switch (unroll) {
+      case 1:
+        return bdl_adam_kernel<NOISE, COLLECT, false, 1>;
+      case 4:
+        return bdl_adam_kernel<NOISE, COLLECT, false, 4>;
+      default:
+        return bdl_adam_kernel<NOISE, COLLECT, false, 2>;
+    }
+  }
+}
+
 template <int NOISE>
-StepKernel pick_adam_collect(int collect, bool grad_only) {
-  if (grad_only) return collect == BDL_COLLECT_NONE ? bdl_adam_kernel<NOISE, BDL_COLLECT_NONE, true> : nullptr;
+StepKernel pick_adam_collect(int collect, bool grad_only, int unroll) {
+  if (grad_only)
+    return collect == BDL_COLLECT_NONE ? bdl_adam_kernel<NOISE, BDL_COLLECT_NONE, true, 2> : nullptr;
   switch (collect) {
     case BDL_COLLECT_NONE:
-      return bdl_adam_kernel<NOISE, BDL_COLLECT_NONE, false>;
+      return pick_adam_unroll<NOISE, BDL_COLLECT_NONE>(unroll);
     case BDL_COLLECT_MEAN_INIT:
-      return bdl_adam_kernel<NOISE, BDL_COLLECT_MEAN_INIT, false>;
+      return pick_adam_unroll<NOISE, BDL_COLLECT_MEAN_INIT>(unroll);
     case BDL_COLLECT_MEAN:
-      return bdl_adam_kernel<NOISE, BDL_COLLECT_MEAN, false>;
+      return pick_adam_unroll<NOISE, BDL_COLLECT_MEAN>(unroll);
   }
   return nullptr;  // the Adam runners collect running means only
 }
 
-StepKernel pick_adam(int noise, int collect, bool grad_only) {
+StepKernel pick_adam(int noise, int collect, bool grad_only, int unroll) {
   switch (noise) {
     case BDL_NOISE_NONE:
-      return pick_adam_collect<BDL_NOISE_NONE>(collect, grad_only);
+      return pick_adam_collect<BDL_NOISE_NONE>(collect, grad_only, unroll);
     case BDL_NOISE_BUFFER:
-      return pick_adam_collect<BDL_NOISE_BUFFER>(collect, grad_only);
+      return pick_adam_collect<BDL_NOISE_BUFFER>(collect, grad_only, unroll);
     case BDL_NOISE_PHILOX:
-      return pick_adam_collect<BDL_NOISE_PHILOX>(collect, grad_only);
+      return pick_adam_collect<BDL_NOISE_PHILOX>(collect, grad_only, unroll);
   }
   return nullptr;
 }
@@ -1356,7 +1379,8 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
                         ad->adam_m, ad->adam_v, ad->sgd_buf};
   for (const void* p : ptrs)
     if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_adam_step: vector not 16-B aligned");
-  StepKernel k = pick_adam(s->noise_mode, s->collect, grad_only);
+  const int unroll = grad_only ? 2 : g_unroll;
+  StepKernel k = pick_adam(s->noise_mode, s->collect, grad_only, unroll);
   if (!k) return fail(BDL_ERR_ARG, "bdl_adam_step: unsupported noise/collect combination");
 
   KArgs a{};
@@ -1403,7 +1427,8 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
   a.inv_bc1 = recip_or(ad->inv_bias_corr1, ad->bias_corr1);
   a.inv_bc2 = recip_or(ad->inv_bias_corr2, ad->bias_corr2);
   const int64_t ngroups = (s->n + 3) / 4;
-  const int64_t iters = (ngroups + 2 * kBlock - 1) / (2 * kBlock);
+  const int64_t per_iter = (int64_t)kBlock * unroll;
+  const int64_t iters = (ngroups + per_iter - 1) / per_iter;
   const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
   const int grid = (int)std::max<int64_t>(1, std::min(iters, cap));
   hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), (size_t)s->nruns * sizeof(bdl_run),

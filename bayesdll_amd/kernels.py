@@ -185,10 +185,10 @@ def set_launch_config(blocks_per_cu=0, unroll=0, grid_stride=0):
 
 # Launch geometries worth trying on gfx950 (workgroups/CU, float4 groups in
 # flight per lane, grid-stride): the sweep (profiles/round1/kernel_v1) shows the optimum
-# moving between these from one device to the next.  Only the cSGHMC kernel
-# has unroll variants; the others are tuned over workgroups/CU.
-AUTOTUNE_CANDIDATES = ((2, 1, 1), (1, 4, 1), (3, 1, 1), (2, 4, 1), (1, 2, 1))
-AUTOTUNE_CANDIDATES_2 = ((1, 2, 1), (2, 2, 1), (3, 2, 1), (4, 2, 1))
+# moving between these from one device to the next.  The production kernels
+# of every method (cSGHMC; SGLD / SGHMC / Adam with noise) exist at unroll
+# depths 1, 2 and 4.
+AUTOTUNE_CANDIDATES = ((2, 1, 1), (1, 4, 1), (3, 1, 1), (2, 4, 1), (1, 2, 1), (2, 2, 1))
 _TUNED = {}
 
 
@@ -207,7 +207,7 @@ def autotune(n, device=None, reps=6, candidates=None, method="csghmc"):
     dev = torch.device(device) if device is not None else torch.device("cuda",
                                                                         torch.cuda.current_device())
     if candidates is None:
-        candidates = AUTOTUNE_CANDIDATES if method == "csghmc" else AUTOTUNE_CANDIDATES_2
+        candidates = AUTOTUNE_CANDIDATES
     st = FlatState.from_segments([("w", (int(n),))], None, device=dev,
                                  need_prior=method != "csghmc")
     st.theta.zero_()
