@@ -758,22 +758,24 @@ __global__ __launch_bounds__(kBlock) void bdl_adam_kernel(const KArgs a) {
 // Gradient-norm reduction for clip_grad_norm_ (csgld.py:250-251).  The SGLD
 // sampler gradient G = g + prior + noise is recomputed per element (Philox
 // noise is a pure function of its counter, so G is never stored) and
-// sum(G^2) reduced: per-lane fp32 fmaf accumulation, a 64-lane wavefront
-// butterfly (__shfl_xor), the block's 4 wave sums through LDS, one partial per
-// workgroup.  A single-workgroup finalize sums the partials in a fixed order
-// (fp64, deterministic) and writes (total_norm, coef).
+// sum(G^2) reduced: per-lane fp64 accumulation (the fp64 FMA is free next to
+// the HBM stream; an fp32 accumulator over ~4 K elements per lane could drift
+// past the 1e-5 tolerance), a 64-lane wavefront butterfly (__shfl_xor), the
+// block's 4 wave sums through LDS, one fp64 partial per workgroup.  A
+// single-workgroup finalize sums the partials in a fixed order
+// (deterministic) and writes (total_norm, coef).
 // ---------------------------------------------------------------------------
 constexpr int kMaxNormPartials = 2048;
 
-__device__ __forceinline__ float wave_sum(float v) {
+__device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
 
 template <int NOISE, bool RECIP, bool PRIOR>
-__device__ __forceinline__ float sqnorm_fast(const KArgs& a, const StepConst& c, int64_t gb,
-                                             float ns, float acc) {
+__device__ __forceinline__ double sqnorm_fast(const KArgs& a, const StepConst& c, int64_t gb,
+                                              float ns, double acc) {
   constexpr int U = 2;
   f4v th[U], g[U], t0[U], ep[U];
   const f4v z = {0.f, 0.f, 0.f, 0.f};
@@ -795,15 +797,15 @@ __device__ __forceinline__ float sqnorm_fast(const KArgs& a, const StepConst& c,
       float xt = th[u][j], xg = g[u][j], xv = 0.f;
       update_core<BDL_SGLD_GRAD, NOISE, RECIP, PRIOR, false>(a, c, 0.f, ns, xt, xg, xv, t0[u][j],
                                                              ep[u][j]);
-      acc = fmaf(xg, xg, acc);
+      acc = fma((double)xg, (double)xg, acc);
     }
   }
   return acc;
 }
 
 template <int NOISE, bool RECIP>
-__device__ __forceinline__ void sqnorm_body(const KArgs& a, float* __restrict__ partials) {
-  __shared__ float s_wave[kBlock / 64];
+__device__ __forceinline__ void sqnorm_body(const KArgs& a, double* __restrict__ partials) {
+  __shared__ double s_wave[kBlock / 64];
   constexpr int64_t kIter = (int64_t)kBlock * 2;
   StepConst c;
   c.sgd_mom = c.sgd_mom_read = c.has_m2 = c.grad_ready = c.clip = false;
@@ -813,7 +815,7 @@ __device__ __forceinline__ void sqnorm_body(const KArgs& a, float* __restrict__ 
   const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
   for (int i = threadIdx.x; i < a.nruns; i += kBlock) s_runs[i] = a.runs[i];
   __syncthreads();
-  float acc = 0.f;
+  double acc = 0.0;
   int r = find_run_lds(a.nruns, (int64_t)blockIdx.x * kIter * 4);
   for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {
     while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
@@ -846,7 +848,7 @@ __device__ __forceinline__ void sqnorm_body(const KArgs& a, float* __restrict__ 
             update_core<BDL_SGLD_GRAD, NOISE, RECIP, true, false>(a, c, 0.f, ns, xt, xg, xv, t0[j], ep[j]);
           else
             update_core<BDL_SGLD_GRAD, NOISE, RECIP, false, false>(a, c, 0.f, ns, xt, xg, xv, t0[j], ep[j]);
-          acc = fmaf(xg, xg, acc);
+          acc = fma((double)xg, (double)xg, acc);
         }
       }
     }
@@ -855,7 +857,7 @@ __device__ __forceinline__ void sqnorm_body(const KArgs& a, float* __restrict__ 
   if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
-    float t = 0.f;
+    double t = 0.0;
 #pragma unroll
     for (int w = 0; w < kBlock / 64; ++w) t += s_wave[w];
     partials[blockIdx.x] = t;
@@ -863,19 +865,19 @@ __device__ __forceinline__ void sqnorm_body(const KArgs& a, float* __restrict__ 
 }
 
 template <int NOISE>
-__global__ __launch_bounds__(kBlock) void bdl_sqnorm_kernel(const KArgs a, float* partials) {
+__global__ __launch_bounds__(kBlock) void bdl_sqnorm_kernel(const KArgs a, double* partials) {
   if (a.flags & BDL_FLAG_RECIP_DIV)
     sqnorm_body<NOISE, true>(a, partials);
   else
     sqnorm_body<NOISE, false>(a, partials);
 }
 
-__global__ __launch_bounds__(kBlock) void bdl_clip_finalize_kernel(const float* __restrict__ partials,
+__global__ __launch_bounds__(kBlock) void bdl_clip_finalize_kernel(const double* __restrict__ partials,
                                                                    int nparts, float max_norm,
                                                                    float* __restrict__ out) {
   __shared__ double s_d[kBlock / 64];
   double acc = 0.0;
-  for (int i = threadIdx.x; i < nparts; i += kBlock) acc += (double)partials[i];
+  for (int i = threadIdx.x; i < nparts; i += kBlock) acc += partials[i];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
   if ((threadIdx.x & 63) == 0) s_d[threadIdx.x >> 6] = acc;
@@ -1282,7 +1284,8 @@ int bdl_sgmcmc_step(const bdl_step_args* s, void* stream) {
 
 int64_t bdl_clip_workspace_bytes(int64_t n) {
   (void)n;
-  return (int64_t)(4 + kMaxNormPartials) * (int64_t)sizeof(float);
+  // (total_norm, coef) + pad to 16 B, then one fp64 partial per workgroup
+  return (int64_t)16 + (int64_t)kMaxNormPartials * (int64_t)sizeof(double);
 }
 
 int bdl_sgld_step_clipped(const bdl_step_args* s, float max_norm, void* workspace, void* stream) {
@@ -1306,7 +1309,7 @@ int bdl_sgld_step_clipped(const bdl_step_args* s, float max_norm, void* workspac
     return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: noise buffer is required");
   hipStream_t st = (hipStream_t)stream;
   float* ws = (float*)workspace;
-  float* partials = ws + 4;
+  double* partials = reinterpret_cast<double*>(reinterpret_cast<char*>(workspace) + 16);
 
   KArgs a{};
   a.theta = s->theta;
