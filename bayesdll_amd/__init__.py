@@ -10,7 +10,7 @@ Drop-in modules (same Runner/Model interfaces as the reference's methods/*.py):
     bayesdll_amd.cyclical CyclicalSGMCMC  (methods/cyclical.py)
 
 The per-step update runs in hand-written HIP kernels for gfx950
-(bayesdll_amd/csrc/bdl_sgmcmc.hip) behind the C-ABI in include/bdl_sgmcmc.h,
+(bayesdll_amd/csrc/, one translation unit per kernel family) behind the C-ABI in include/bdl_sgmcmc.h,
 loaded with ctypes.  There is no CPU path: without a HIP device or without the
 built library, the samplers raise.
 """

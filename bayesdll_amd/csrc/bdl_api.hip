@@ -1,0 +1,712 @@
+// bdl_api.hip — fused SG-MCMC parameter update for MI355X (gfx950, CDNA4).
+//
+// One bandwidth-bound sweep over flat fp32 vectors (parameters_to_vector order)
+// replaces the reference's per-tensor update loops plus torch.optim.SGD.step()
+// plus the thinned posterior-moment accumulation:
+//   cSGHMC  methods/csghmc.py:747-778  (+ Welford collect :327-345)
+//   SGHMC   methods/sghmc.py:482-510   (+ SGD momentum 0, :229; moments :242-249)
+//   SGLD    methods/sgld.py:469-484    (+ SGD momentum mu, :226; moments :239-246)
+//   cSGLD   methods/csgld.py:665-680   (+ SGD, :253; per-cycle moments :280-293)
+//
+// Design:
+//   * elementwise, HBM-bound: no LDS on the data stream, no MFMA; 16-B (dwordx4)
+//     loads/stores per lane, several independent float4 groups in flight per
+//     lane, each workgroup sweeps one contiguous span of the vector.
+//   * per-element attributes (lr group, prior on/off, skip) come from a tiny
+//     sorted run table; a block finds its first run with a block-uniform
+//     (scalar) binary search and each lane advances a cursor monotonically.
+//   * noise: either read from a buffer (torch-RNG parity mode) or generated in
+//     registers by counter-based Philox4x32-10 keyed by (seed, chain, step,
+//     element/4) + Box-Muller on v_log/v_sin/v_cos — no extra HBM traffic.
+//   * every floating-point op is rounded separately in the reference's order
+//     (compiled with -ffp-contract=off); SGD's add(alpha=-lr) is an explicit
+//     fmaf, as torch's CPU kernel computes it.
+//
+// Files: bdl_kernels.hpp (device code shared by the kernel families),
+// bdl_step_{csghmc,sghmc,sgld}.hip and bdl_adam.hip (kernel instances per
+// method, compiled in parallel), this file (host entry points of the C-ABI,
+// validation, launch geometry, the clip-norm / moments / sample kernels).
+#include "bdl_kernels.hpp"
+
+namespace bdl {
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* msg) {
+  g_last_error = msg;
+  return code;
+}
+
+// Tunables (bdl_set_launch_config).  blocks_per_cu * 256 CUs workgroups, each
+// lane keeps kUnroll float4 groups in flight per iteration.
+// Defaults from the gfx950 sweep (tools/sweep.py, profiles/round1/kernel_v1/sweep_*.log):
+// grid-stride with 2 workgroups/CU and 1 float4 group in flight per lane,
+// non-temporal 16-B loads and stores, measured best on every kernel kind.
+int g_blocks_per_cu = 2;
+int g_unroll = 1;
+int g_grid_stride = 1;  // 0: one contiguous span per block; 1: grid-stride sweep
+
+int device_cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cached[dev] = cus;
+  }
+  return cached[dev];
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// ---------------------------------------------------------------------------
+// Gradient-norm reduction for clip_grad_norm_ (csgld.py:250-251).  The SGLD
+// sampler gradient G = g + prior + noise is recomputed per element (Philox
+// noise is a pure function of its counter, so G is never stored) and
+// sum(G^2) reduced: per-lane fp64 accumulation (the fp64 FMA is free next to
+// the HBM stream; an fp32 accumulator over ~4 K elements per lane could drift
+// past the 1e-5 tolerance), a 64-lane wavefront butterfly (__shfl_xor), the
+// block's 4 wave sums through LDS, one fp64 partial per workgroup.  A
+// single-workgroup finalize sums the partials in a fixed order
+// (deterministic) and writes (total_norm, coef).
+// ---------------------------------------------------------------------------
+constexpr int kMaxNormPartials = 2048;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int NOISE, bool RECIP, bool PRIOR>
+__device__ __forceinline__ double sqnorm_fast(const KArgs& a, const StepConst& c, int64_t gb,
+                                              float ns, double acc) {
+  constexpr int U = 2;
+  f4v th[U], g[U], t0[U], ep[U];
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+    t0[u] = ep[u] = z;
+    th[u] = vload(a.theta + e);
+    g[u] = vload(a.grad + e);
+    if constexpr (PRIOR) t0[u] = vload(a.prior_mean + e);
+    if constexpr (NOISE == BDL_NOISE_BUFFER) ep[u] = vload(a.noise + e);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float xt = th[u][j], xg = g[u][j], xv = 0.f;
+      update_core<BDL_SGLD_GRAD, NOISE, RECIP, PRIOR, false>(a, c, 0.f, ns, xt, xg, xv, t0[u][j],
+                                                             ep[u][j]);
+      acc = fma((double)xg, (double)xg, acc);
+    }
+  }
+  return acc;
+}
+
+template <int NOISE, bool RECIP>
+__device__ __forceinline__ void sqnorm_body(const KArgs& a, double* __restrict__ partials) {
+  __shared__ double s_wave[kBlock / 64];
+  constexpr int64_t kIter = (int64_t)kBlock * 2;
+  StepConst c;
+  c.sgd_mom = c.sgd_mom_read = c.has_m2 = c.grad_ready = c.clip = false;
+  c.inv_s2 = a.inv_s2;
+  c.inv_nd = a.inv_nd;
+  c.inv_ca = c.inv_cb = c.clip_coef = 1.0f;
+  const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
+  for (int i = threadIdx.x; i < a.nruns; i += kBlock) s_runs[i] = a.runs[i];
+  __syncthreads();
+  double acc = 0.0;
+  int r = find_run_lds(a.nruns, (int64_t)blockIdx.x * kIter * 4);
+  for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {
+    while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
+    const int64_t gend = min(gb + kIter, ngroups);
+    const uint32_t attr = run_attr(r);
+    if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 && !(attr & BDL_ATTR_SKIP)) {
+      const float ns = (attr & BDL_ATTR_HEAD) ? a.ns1 : a.ns0;
+      if (attr & BDL_ATTR_PRIOR)
+        acc = sqnorm_fast<NOISE, RECIP, true>(a, c, gb, ns, acc);
+      else
+        acc = sqnorm_fast<NOISE, RECIP, false>(a, c, gb, ns, acc);
+    } else {
+      for (int u = 0; u < 2; ++u) {
+        const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+        if (gi >= gend) continue;
+        const int64_t e = gi * 4;
+        const f4v z = {0.f, 0.f, 0.f, 0.f};
+        const f4v th = ld4(a.theta, e, a.n), g = ld4(a.grad, e, a.n);
+        const f4v t0 = ld4(a.prior_mean, e, a.n);
+        f4v ep = z;
+        if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, a.n);
+        if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+        for (int j = 0; j < 4; ++j) {
+          if (e + j >= a.n) break;
+          const uint32_t at = run_attr(find_run_lds(a.nruns, e + j));
+          if (at & BDL_ATTR_SKIP) continue;  // .grad is None: not in the norm
+          float xt = th[j], xg = g[j], xv = 0.f;
+          const float ns = (at & BDL_ATTR_HEAD) ? a.ns1 : a.ns0;
+          if (at & BDL_ATTR_PRIOR)
+            update_core<BDL_SGLD_GRAD, NOISE, RECIP, true, false>(a, c, 0.f, ns, xt, xg, xv, t0[j], ep[j]);
+          else
+            update_core<BDL_SGLD_GRAD, NOISE, RECIP, false, false>(a, c, 0.f, ns, xt, xg, xv, t0[j], ep[j]);
+          acc = fma((double)xg, (double)xg, acc);
+        }
+      }
+    }
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) t += s_wave[w];
+    partials[blockIdx.x] = t;
+  }
+}
+
+template <int NOISE>
+__global__ __launch_bounds__(kBlock) void bdl_sqnorm_kernel(const KArgs a, double* partials) {
+  if (a.flags & BDL_FLAG_RECIP_DIV)
+    sqnorm_body<NOISE, true>(a, partials);
+  else
+    sqnorm_body<NOISE, false>(a, partials);
+}
+
+__global__ __launch_bounds__(kBlock) void bdl_clip_finalize_kernel(const double* __restrict__ partials,
+                                                                   int nparts, float max_norm,
+                                                                   float* __restrict__ out) {
+  __shared__ double s_d[kBlock / 64];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += kBlock) acc += partials[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if ((threadIdx.x & 63) == 0) s_d[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < kBlock / 64; ++w) t += s_d[w];
+    const float norm = (float)sqrt(t);
+    // clip_grad_norm_: clip_coef = max_norm / (total_norm + 1e-6) (Tensor.__rtruediv__
+    // = reciprocal() * other), clamped at 1.0
+    float coef = (1.0f / (norm + 1e-6f)) * max_norm;
+    coef = fminf(coef, 1.0f);
+    out[0] = norm;
+    out[1] = coef;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Stand-alone moments, posterior sample, raw Philox stream.
+// ---------------------------------------------------------------------------
+struct MArgs {
+  const float* __restrict__ theta;
+  float* __restrict__ mom1;
+  float* __restrict__ mom2;
+  int64_t n;
+  int32_t collect;
+  int32_t recip;
+  float ca, cb, inv_ca, inv_cb;
+};
+
+__global__ __launch_bounds__(kBlock) void bdl_moments_kernel(const MArgs a) {
+  const int64_t ngroups = (a.n + 3) >> 2;
+  const float inv_ca = a.inv_ca, inv_cb = a.inv_cb;
+  for (int64_t gi = (int64_t)blockIdx.x * kBlock + threadIdx.x; gi < ngroups;
+       gi += (int64_t)gridDim.x * kBlock) {
+    const int64_t e = gi * 4;
+    const f4v t = ld4(a.theta, e, a.n);
+    f4v m1 = {0.f, 0.f, 0.f, 0.f}, m2 = m1;
+    if (a.collect == BDL_COLLECT_WELFORD || a.collect == BDL_COLLECT_MEAN) {
+      m1 = ld4(a.mom1, e, a.n);
+      if (a.mom2) m2 = ld4(a.mom2, e, a.n);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = t[j];
+      float p = m1[j], q = m2[j];
+      switch (a.collect) {
+        case BDL_COLLECT_WELFORD_INIT:
+          p = x;
+          q = 0.f;
+          break;
+        case BDL_COLLECT_WELFORD: {
+          const float d = x - p;
+          p = p + (a.recip ? d * inv_ca : d / a.ca);
+          const float d2 = x - p;
+          q = q + d * d2;
+          break;
+        }
+        case BDL_COLLECT_MEAN_INIT:
+          p = x;
+          q = x * x;
+          break;
+        default: {  // MEAN
+          const float u = x + a.ca * p;
+          p = a.recip ? u * inv_cb : u / a.cb;
+          const float w = x * x + a.ca * q;
+          q = a.recip ? w * inv_cb : w / a.cb;
+        }
+      }
+      m1[j] = p;
+      m2[j] = q;
+    }
+    st4(a.mom1, e, a.n, m1);
+    if (a.mom2) st4(a.mom2, e, a.n, m2);
+  }
+}
+
+struct SArgs {
+  float* __restrict__ out;
+  const float* __restrict__ mom1;
+  const float* __restrict__ mom2;
+  const float* __restrict__ noise;
+  int64_t n;
+  int32_t var_mode, noise_mode;
+  float ratio, var_floor, inv_ratio;
+  uint64_t seed, chain, step;
+};
+
+__global__ __launch_bounds__(kBlock) void bdl_sample_kernel(const SArgs a) {
+  const int64_t ngroups = (a.n + 3) >> 2;
+  for (int64_t gi = (int64_t)blockIdx.x * kBlock + threadIdx.x; gi < ngroups;
+       gi += (int64_t)gridDim.x * kBlock) {
+    const int64_t e = gi * 4;
+    const f4v m = ld4(a.mom1, e, a.n);
+    f4v q = {0.f, 0.f, 0.f, 0.f};
+    if (a.mom2) q = ld4(a.mom2, e, a.n);
+    const f4v eps = (a.noise_mode == BDL_NOISE_BUFFER)
+                        ? ld4(a.noise, e, a.n)
+                        : philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+    f4v o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float mj = m[j];
+      const float qj = q[j];
+      float var;
+      if (!a.mom2)
+        var = a.var_floor;  // single-sample cycle: ones*1e-12 (csghmc.py:456-458)
+      else if (a.var_mode == BDL_VAR_RAW_MOMENTS)
+        var = a.ratio * (qj - mj * mj);  // sgld.py:342
+      else if (a.var_mode == BDL_VAR_WELFORD)
+        var = a.inv_ratio != 0.0f ? qj * a.inv_ratio : qj / a.ratio;  // csghmc.py:455
+      else
+        var = qj;
+      if (!(var != var)) var = fmaxf(var, a.var_floor);  // clamp_(min=1e-12); NaN stays NaN
+      o[j] = mj + sqrtf(var) * eps[j];  // p_m + p_v.sqrt()*eps
+    }
+    st4(a.out, e, a.n, o);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void bdl_philox_kernel(float* __restrict__ out, int64_t n,
+                                                            uint64_t seed, uint64_t chain,
+                                                            uint64_t step) {
+  const int64_t ngroups = (n + 3) >> 2;
+  for (int64_t gi = (int64_t)blockIdx.x * kBlock + threadIdx.x; gi < ngroups;
+       gi += (int64_t)gridDim.x * kBlock) {
+    st4(out, gi * 4, n, philox_normal4((uint64_t)gi, seed, chain, step));
+  }
+}
+
+StepKernel pick_step(int method, int noise, int collect, int unroll) {
+  switch (method) {
+    case BDL_CSGHMC:
+      return pick_step_csghmc(noise, collect, unroll);
+    case BDL_SGHMC:
+    case BDL_SGHMC_GRAD:
+      return pick_step_sghmc(method, noise, collect, unroll);
+    case BDL_SGLD:
+    case BDL_SGLD_GRAD:
+      return pick_step_sgld(method, noise, collect, unroll);
+  }
+  return nullptr;
+}
+
+int grid_for(int64_t ngroups, int per_block_groups) {
+  const int64_t want = (ngroups + per_block_groups - 1) / per_block_groups;
+  const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
+  return (int)std::max<int64_t>(1, std::min(want, cap));
+}
+
+// Validate a step descriptor, pick the kernel instance and launch it; `clip`
+// (device pointer to (norm, coef)) scales the SGLD sampler gradient when set.
+int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
+  if (!s) return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: null args");
+  if (s->n < 0) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: n < 0");
+  if (s->method < BDL_CSGHMC || s->method > BDL_SGLD_GRAD)
+    return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: unknown method");
+  if (s->noise_mode < BDL_NOISE_NONE || s->noise_mode > BDL_NOISE_PHILOX)
+    return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: unknown noise mode");
+  if (s->collect < BDL_COLLECT_NONE || s->collect > BDL_COLLECT_MEAN)
+    return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: unknown collect mode");
+  if (s->n == 0) return BDL_OK;
+  const bool grad_only = s->method == BDL_SGHMC_GRAD || s->method == BDL_SGLD_GRAD;
+  const bool needs_mom = s->method == BDL_CSGHMC || s->method == BDL_SGHMC ||
+                         s->method == BDL_SGHMC_GRAD ||
+                         (s->method == BDL_SGLD && (s->flags & BDL_FLAG_MOMENTUM));
+  const bool needs_prior = s->method != BDL_CSGHMC;
+  if (!s->theta || !s->grad || !s->runs || s->nruns < 1)
+    return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: theta, grad and runs are required");
+  if (s->nruns > kMaxRuns)
+    return fail(BDL_ERR_RUNS, "bdl_sgmcmc_step: more than 4096 runs (merge parameter groups)");
+  if (needs_mom && !s->mom) return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: mom is required");
+  if (needs_prior && !s->prior_mean)
+    return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: prior_mean is required for sghmc/sgld");
+  if (s->noise_mode == BDL_NOISE_BUFFER && !s->noise)
+    return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: noise buffer is required");
+  if (s->collect != BDL_COLLECT_NONE && !s->mom1)
+    return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: mom1 is required to collect");
+  if (grad_only && s->collect != BDL_COLLECT_NONE)
+    return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: grad-only methods cannot collect");
+  const void* ptrs[] = {s->theta, s->grad, s->mom, s->prior_mean, s->noise, s->mom1, s->mom2};
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_sgmcmc_step: vector not 16-B aligned");
+
+  const int unroll = g_unroll;
+  StepKernel k = pick_step(s->method, s->noise_mode, s->collect, unroll);
+  if (!k) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: unsupported method/noise/collect combination");
+
+  const int64_t ngroups = (s->n + 3) / 4;
+  const int64_t per_iter = (int64_t)kBlock * unroll;
+  const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
+  int64_t iters = (ngroups + per_iter - 1) / per_iter;
+  int64_t grid = std::max<int64_t>(1, std::min(iters, cap));
+  int64_t iters_per_block = (iters + grid - 1) / grid;
+  grid = (iters + iters_per_block - 1) / iters_per_block;
+
+  KArgs a;
+  a.theta = s->theta;
+  a.grad = s->grad;
+  a.mom = s->mom;
+  a.prior_mean = s->prior_mean;
+  a.noise = s->noise;
+  a.mom1 = s->mom1;
+  a.mom2 = s->mom2;
+  a.runs = s->runs;
+  a.nruns = s->nruns;
+  a.flags = s->flags;
+  a.n = s->n;
+  a.groups_per_block = g_grid_stride ? 0 : iters_per_block * per_iter;
+  a.lr0 = s->lr[0];
+  a.lr1 = s->lr[1];
+  a.ns0 = s->noise_scale[0];
+  a.ns1 = s->noise_scale[1];
+  a.one_minus_alpha = s->one_minus_alpha;
+  a.prior_sig = s->prior_sig;
+  a.sigma2 = s->sigma2;
+  a.n_data = s->n_data;
+  a.mu = s->mu;
+  a.ca = s->collect_a;
+  a.cb = s->collect_b;
+  a.seed = s->seed;
+  a.chain = s->chain;
+  a.step = s->step;
+  a.clip = clip;
+  a.inv_s2 = recip_or(s->inv_sigma2, s->sigma2);
+  a.inv_nd = recip_or(s->inv_n_data, s->n_data);
+  a.inv_ca = recip_or(s->inv_collect_a, s->collect_a);
+  a.inv_cb = recip_or(s->inv_collect_b, s->collect_b);
+
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kBlock), (size_t)s->nruns * sizeof(bdl_run),
+                     stream, a);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    g_last_error = std::string("bdl_sgmcmc_step: launch failed: ") + hipGetErrorString(err);
+    return BDL_ERR_LAUNCH;
+  }
+  return BDL_OK;
+}
+
+}  // namespace
+}  // namespace bdl
+
+using namespace bdl;
+
+extern "C" {
+
+int bdl_version(void) { return BDL_ABI_VERSION; }
+
+const char* bdl_last_error(void) { return g_last_error.c_str(); }
+
+int bdl_set_launch_config(int32_t blocks_per_cu, int32_t unroll, int32_t grid_stride) {
+  const int prev = (g_grid_stride << 24) | (g_blocks_per_cu << 8) | g_unroll;
+  g_blocks_per_cu = blocks_per_cu > 0 ? blocks_per_cu : 2;
+  g_unroll = (unroll == 1 || unroll == 2 || unroll == 4) ? unroll : 1;
+  g_grid_stride = grid_stride > 0 ? 1 : 0;
+  return prev;
+}
+
+int bdl_build_runs(const bdl_segment* segs, int32_t nseg, int64_t n, bdl_run* out, int32_t max_runs) {
+  if (!out || (nseg > 0 && !segs)) return fail(BDL_ERR_NULL, "bdl_build_runs: null pointer");
+  if (n < 0 || nseg < 0 || max_runs < 1) return fail(BDL_ERR_ARG, "bdl_build_runs: bad sizes");
+  int nr = 0;
+  int64_t pos = 0;
+  auto push = [&](int64_t end, uint32_t attr) -> bool {
+    if (end <= pos) return true;
+    if (nr > 0 && out[nr - 1].attr == attr) {
+      out[nr - 1].end = end;
+    } else {
+      if (nr >= max_runs) return false;
+      out[nr].end = end;
+      out[nr].attr = attr;
+      out[nr].pad = 0;
+      ++nr;
+    }
+    pos = end;
+    return true;
+  };
+  for (int i = 0; i < nseg; ++i) {
+    const bdl_segment& s = segs[i];
+    if (s.offset < pos || s.numel < 0 || s.offset + s.numel > n)
+      return fail(BDL_ERR_RUNS, "bdl_build_runs: segments overlap, are unsorted or exceed n");
+    if (!push(s.offset, BDL_ATTR_SKIP)) return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
+    if (!push(s.offset + s.numel, s.attr & 7u))
+      return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
+  }
+  if (!push(n, BDL_ATTR_SKIP)) return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
+  if (nr == 0) {  // n == 0: one empty run keeps the table well-formed
+    out[0].end = 0;
+    out[0].attr = BDL_ATTR_SKIP;
+    out[0].pad = 0;
+    nr = 1;
+  }
+  return nr;
+}
+
+int bdl_sgmcmc_step(const bdl_step_args* s, void* stream) {
+  return launch_step(s, nullptr, (hipStream_t)stream);
+}
+
+int64_t bdl_clip_workspace_bytes(int64_t n) {
+  (void)n;
+  // (total_norm, coef) + pad to 16 B, then one fp64 partial per workgroup
+  return (int64_t)16 + (int64_t)kMaxNormPartials * (int64_t)sizeof(double);
+}
+
+int bdl_sgld_step_clipped(const bdl_step_args* s, float max_norm, void* workspace, void* stream) {
+  if (!s) return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: null args");
+  if (!workspace) return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: null workspace");
+  if (!aligned16(workspace)) return fail(BDL_ERR_ALIGN, "bdl_sgld_step_clipped: workspace not 16-B aligned");
+  if (s->method != BDL_SGLD)
+    return fail(BDL_ERR_ARG, "bdl_sgld_step_clipped: only the SGLD sampler clips its gradient");
+  if (s->flags & BDL_FLAG_GRAD_READY)
+    return fail(BDL_ERR_ARG, "bdl_sgld_step_clipped: GRAD_READY is incompatible with clipping");
+  if (!(max_norm > 0.0f)) return fail(BDL_ERR_ARG, "bdl_sgld_step_clipped: max_norm must be > 0");
+  if (s->n < 0) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: n < 0");
+  if (s->n == 0) return BDL_OK;
+  if (s->noise_mode < BDL_NOISE_NONE || s->noise_mode > BDL_NOISE_PHILOX)
+    return fail(BDL_ERR_ARG, "bdl_sgld_step_clipped: unknown noise mode");
+  if (!s->theta || !s->grad || !s->runs || !s->prior_mean || s->nruns < 1)
+    return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: theta, grad, prior_mean and runs are required");
+  if (s->nruns > kMaxRuns)
+    return fail(BDL_ERR_RUNS, "bdl_sgld_step_clipped: more than 4096 runs (merge parameter groups)");
+  if (s->noise_mode == BDL_NOISE_BUFFER && !s->noise)
+    return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: noise buffer is required");
+  hipStream_t st = (hipStream_t)stream;
+  float* ws = (float*)workspace;
+  double* partials = reinterpret_cast<double*>(reinterpret_cast<char*>(workspace) + 16);
+
+  KArgs a{};
+  a.theta = s->theta;
+  a.grad = s->grad;
+  a.prior_mean = s->prior_mean;
+  a.noise = s->noise;
+  a.runs = s->runs;
+  a.nruns = s->nruns;
+  a.flags = s->flags;
+  a.n = s->n;
+  a.ns0 = s->noise_scale[0];
+  a.ns1 = s->noise_scale[1];
+  a.sigma2 = s->sigma2;
+  a.n_data = s->n_data;
+  a.seed = s->seed;
+  a.chain = s->chain;
+  a.step = s->step;
+  a.inv_s2 = recip_or(s->inv_sigma2, s->sigma2);
+  a.inv_nd = recip_or(s->inv_n_data, s->n_data);
+  const int64_t ngroups = (s->n + 3) / 4;
+  const int64_t iters = (ngroups + 2 * kBlock - 1) / (2 * kBlock);
+  const int64_t cap = std::min<int64_t>((int64_t)device_cu_count() * g_blocks_per_cu, kMaxNormPartials);
+  const int grid = (int)std::max<int64_t>(1, std::min(iters, cap));
+  const size_t shmem = (size_t)s->nruns * sizeof(bdl_run);
+  switch (s->noise_mode) {
+    case BDL_NOISE_NONE:
+      hipLaunchKernelGGL(bdl_sqnorm_kernel<BDL_NOISE_NONE>, dim3(grid), dim3(kBlock), shmem, st, a, partials);
+      break;
+    case BDL_NOISE_BUFFER:
+      hipLaunchKernelGGL(bdl_sqnorm_kernel<BDL_NOISE_BUFFER>, dim3(grid), dim3(kBlock), shmem, st, a, partials);
+      break;
+    default:
+      hipLaunchKernelGGL(bdl_sqnorm_kernel<BDL_NOISE_PHILOX>, dim3(grid), dim3(kBlock), shmem, st, a, partials);
+      break;
+  }
+  hipLaunchKernelGGL(bdl_clip_finalize_kernel, dim3(1), dim3(kBlock), 0, st, partials, grid, max_norm, ws);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    g_last_error = std::string("bdl_sgld_step_clipped: launch failed: ") + hipGetErrorString(err);
+    return BDL_ERR_LAUNCH;
+  }
+  return launch_step(s, ws, st);
+}
+
+int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream) {
+  if (!s || !ad) return fail(BDL_ERR_NULL, "bdl_adam_step: null args");
+  if (s->method != BDL_ADAM_SGHMC && s->method != BDL_ADAM_SGHMC_GRAD)
+    return fail(BDL_ERR_ARG, "bdl_adam_step: method must be BDL_ADAM_SGHMC or BDL_ADAM_SGHMC_GRAD");
+  if (s->noise_mode < BDL_NOISE_NONE || s->noise_mode > BDL_NOISE_PHILOX)
+    return fail(BDL_ERR_ARG, "bdl_adam_step: unknown noise mode");
+  if (s->collect < BDL_COLLECT_NONE || s->collect > BDL_COLLECT_MEAN)
+    return fail(BDL_ERR_ARG, "bdl_adam_step: unknown collect mode");
+  if (s->n < 0) return fail(BDL_ERR_ARG, "bdl_adam_step: n < 0");
+  if (s->n == 0) return BDL_OK;
+  const bool grad_only = s->method == BDL_ADAM_SGHMC_GRAD;
+  if (!s->theta || !s->grad || !s->mom || !s->prior_mean || !ad->adam_m || !ad->adam_v ||
+      !s->runs || s->nruns < 1)
+    return fail(BDL_ERR_NULL, "bdl_adam_step: theta, grad, mom, prior_mean, adam_m, adam_v and runs are required");
+  if (s->nruns > kMaxRuns)
+    return fail(BDL_ERR_RUNS, "bdl_adam_step: more than 4096 runs (merge parameter groups)");
+  if (!grad_only && (s->flags & BDL_FLAG_MOMENTUM) && !ad->sgd_buf)
+    return fail(BDL_ERR_NULL, "bdl_adam_step: sgd_buf is required with BDL_FLAG_MOMENTUM");
+  if (s->noise_mode == BDL_NOISE_BUFFER && !s->noise)
+    return fail(BDL_ERR_NULL, "bdl_adam_step: noise buffer is required");
+  if (s->collect != BDL_COLLECT_NONE && !s->mom1)
+    return fail(BDL_ERR_NULL, "bdl_adam_step: mom1 is required to collect");
+  if (s->flags & BDL_FLAG_GRAD_READY)
+    return fail(BDL_ERR_ARG, "bdl_adam_step: GRAD_READY is not an Adam flag (use bdl_sgmcmc_step)");
+  const void* ptrs[] = {s->theta, s->grad, s->mom, s->prior_mean, s->noise, s->mom1, s->mom2,
+                        ad->adam_m, ad->adam_v, ad->sgd_buf};
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_adam_step: vector not 16-B aligned");
+  const int unroll = grad_only ? 2 : g_unroll;
+  StepKernel k = pick_adam(s->noise_mode, s->collect, grad_only, unroll);
+  if (!k) return fail(BDL_ERR_ARG, "bdl_adam_step: unsupported noise/collect combination");
+
+  KArgs a{};
+  a.theta = s->theta;
+  a.grad = s->grad;
+  a.mom = s->mom;
+  a.prior_mean = s->prior_mean;
+  a.noise = s->noise;
+  a.mom1 = s->mom1;
+  a.mom2 = s->mom2;
+  a.runs = s->runs;
+  a.nruns = s->nruns;
+  a.flags = (s->flags & ~kFlagGradIsMom) | (ad->grad_is_mom ? kFlagGradIsMom : 0);
+  a.n = s->n;
+  a.lr0 = s->lr[0];
+  a.lr1 = s->lr[1];
+  a.one_minus_alpha = s->one_minus_alpha;
+  a.sigma2 = s->sigma2;
+  a.n_data = s->n_data;
+  a.mu = s->mu;
+  a.ca = s->collect_a;
+  a.cb = s->collect_b;
+  a.seed = s->seed;
+  a.chain = s->chain;
+  a.step = s->step;
+  a.adam_m = ad->adam_m;
+  a.adam_v = ad->adam_v;
+  a.sgd_buf = ad->sgd_buf;
+  a.b1 = ad->beta1;
+  a.omb1 = ad->one_minus_beta1;
+  a.b2 = ad->beta2;
+  a.omb2 = ad->one_minus_beta2;
+  a.bc1 = ad->bias_corr1;
+  a.bc2 = ad->bias_corr2;
+  a.aeps = ad->eps;
+  a.two_alpha = ad->two_alpha;
+  a.nd = ad->nd;
+  a.temp = ad->temperature;
+  a.inv_s2 = recip_or(s->inv_sigma2, s->sigma2);
+  a.inv_nd = recip_or(s->inv_n_data, s->n_data);
+  a.inv_ca = recip_or(s->inv_collect_a, s->collect_a);
+  a.inv_cb = recip_or(s->inv_collect_b, s->collect_b);
+  a.inv_temp = recip_or(ad->inv_temperature, ad->temperature);
+  a.inv_bc1 = recip_or(ad->inv_bias_corr1, ad->bias_corr1);
+  a.inv_bc2 = recip_or(ad->inv_bias_corr2, ad->bias_corr2);
+  const int64_t ngroups = (s->n + 3) / 4;
+  const int64_t per_iter = (int64_t)kBlock * unroll;
+  const int64_t iters = (ngroups + per_iter - 1) / per_iter;
+  const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
+  const int grid = (int)std::max<int64_t>(1, std::min(iters, cap));
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), (size_t)s->nruns * sizeof(bdl_run),
+                     (hipStream_t)stream, a);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    g_last_error = std::string("bdl_adam_step: launch failed: ") + hipGetErrorString(err);
+    return BDL_ERR_LAUNCH;
+  }
+  return BDL_OK;
+}
+
+int bdl_moments_update(const bdl_moments_args* m, void* stream) {
+  if (!m) return fail(BDL_ERR_NULL, "bdl_moments_update: null args");
+  if (m->n < 0 || m->collect < BDL_COLLECT_WELFORD_INIT || m->collect > BDL_COLLECT_MEAN)
+    return fail(BDL_ERR_ARG, "bdl_moments_update: bad n or collect mode");
+  if (m->n == 0) return BDL_OK;
+  if (!m->theta || !m->mom1) return fail(BDL_ERR_NULL, "bdl_moments_update: theta/mom1 required");
+  const void* ptrs[] = {m->theta, m->mom1, m->mom2};
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_moments_update: vector not 16-B aligned");
+  MArgs a{m->theta, m->mom1, m->mom2, m->n, m->collect, (m->flags & BDL_FLAG_RECIP_DIV) ? 1 : 0,
+          m->collect_a, m->collect_b, recip_or(m->inv_collect_a, m->collect_a),
+          recip_or(m->inv_collect_b, m->collect_b)};
+  hipLaunchKernelGGL(bdl_moments_kernel, dim3(grid_for((m->n + 3) / 4, kBlock * 4)), dim3(kBlock), 0,
+                     (hipStream_t)stream, a);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    g_last_error = std::string("bdl_moments_update: launch failed: ") + hipGetErrorString(err);
+    return BDL_ERR_LAUNCH;
+  }
+  return BDL_OK;
+}
+
+int bdl_posterior_sample(const bdl_sample_args* s, void* stream) {
+  if (!s) return fail(BDL_ERR_NULL, "bdl_posterior_sample: null args");
+  if (s->n < 0 || s->var_mode < BDL_VAR_GIVEN || s->var_mode > BDL_VAR_WELFORD ||
+      (s->noise_mode != BDL_NOISE_BUFFER && s->noise_mode != BDL_NOISE_PHILOX))
+    return fail(BDL_ERR_ARG, "bdl_posterior_sample: bad arguments");
+  if (s->n == 0) return BDL_OK;
+  if (!s->out || !s->mom1 || (s->noise_mode == BDL_NOISE_BUFFER && !s->noise))
+    return fail(BDL_ERR_NULL, "bdl_posterior_sample: out, mom1 (and noise) required");
+  const void* ptrs[] = {s->out, s->mom1, s->mom2, s->noise};
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_posterior_sample: vector not 16-B aligned");
+  SArgs a{s->out, s->mom1, s->mom2, s->noise, s->n, s->var_mode, s->noise_mode,
+          s->ratio, s->var_floor, s->inv_ratio, s->seed, s->chain, s->step};
+  hipLaunchKernelGGL(bdl_sample_kernel, dim3(grid_for((s->n + 3) / 4, kBlock * 4)), dim3(kBlock), 0,
+                     (hipStream_t)stream, a);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    g_last_error = std::string("bdl_posterior_sample: launch failed: ") + hipGetErrorString(err);
+    return BDL_ERR_LAUNCH;
+  }
+  return BDL_OK;
+}
+
+int bdl_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t chain, uint64_t step,
+                      void* stream) {
+  if (n < 0) return fail(BDL_ERR_ARG, "bdl_philox_normal: n < 0");
+  if (n == 0) return BDL_OK;
+  if (!out) return fail(BDL_ERR_NULL, "bdl_philox_normal: null out");
+  if (!aligned16(out)) return fail(BDL_ERR_ALIGN, "bdl_philox_normal: out not 16-B aligned");
+  hipLaunchKernelGGL(bdl_philox_kernel, dim3(grid_for((n + 3) / 4, kBlock * 4)), dim3(kBlock), 0,
+                     (hipStream_t)stream, out, n, seed, chain, step);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    g_last_error = std::string("bdl_philox_normal: launch failed: ") + hipGetErrorString(err);
+    return BDL_ERR_LAUNCH;
+  }
+  return BDL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,770 @@
+// bdl_kernels.hpp — device side of the fused SG-MCMC library (shared by the
+// per-method translation units; see bdl_api.hip for the overview).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+
+#include "bdl_sgmcmc.h"
+
+namespace bdl {
+
+constexpr int kBlock = 256;  // 4 waves of 64 lanes
+
+// ---------------------------------------------------------------------------
+// Counter-based RNG: Philox4x32-10 (Salmon et al., SC'11) + Box-Muller.
+// counter = (group index lo32, chain lo32, step lo32, step hi32), key = seed.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// uniform in (0, 1): 24 random bits, centred in their bucket -> never 0 or 1.
+__device__ __forceinline__ float u01(uint32_t x) {
+  return ((float)(x >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+// Four N(0,1) draws for flat elements 4*group .. 4*group+3.
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4v philox_normal4(uint64_t group, uint64_t seed, uint64_t chain,
+                                               uint64_t step) {
+  const uint4 ctr = make_uint4((uint32_t)group, (uint32_t)chain, (uint32_t)step,
+                               (uint32_t)(step >> 32));
+  const uint4 r = philox4x32_10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+  // v_log_f32 is log2; v_sin_f32 / v_cos_f32 take the angle in revolutions,
+  // so sin(2*pi*u) is one instruction with no range reduction.
+  const float kM2Ln2 = -1.38629436111989061883f;  // -2 ln 2
+  const float ra = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(r.x)));
+  const float rb = __builtin_amdgcn_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(r.z)));
+  const float ta = u01(r.y), tb = u01(r.w);
+  f4v z;
+  z.x = ra * __builtin_amdgcn_cosf(ta);
+  z.y = ra * __builtin_amdgcn_sinf(ta);
+  z.z = rb * __builtin_amdgcn_cosf(tb);
+  z.w = rb * __builtin_amdgcn_sinf(tb);
+  return z;
+}
+
+// ---------------------------------------------------------------------------
+// Vector helpers: a 16-B "group" covers flat elements [4g, 4g+4).  Only the
+// very last group of a vector can be partial; it takes the guarded path.
+// ---------------------------------------------------------------------------
+// 16-B vector access.  Streaming (non-temporal) policy per direction:
+// -DBDL_NT_LOAD / -DBDL_NT_STORE (or -DBDL_NT for both; the default build).
+// Every vector is touched once per step and is far larger than the 256 MiB
+// Infinity Cache, so nothing is lost by not keeping lines resident.
+#ifdef BDL_NT
+#define BDL_NT_LOAD 1
+#define BDL_NT_STORE 1
+#endif
+__device__ __forceinline__ f4v vload(const float* p) {
+#ifdef BDL_NT_LOAD
+  return __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+#else
+  return *reinterpret_cast<const f4v*>(p);
+#endif
+}
+
+__device__ __forceinline__ void vstore(float* p, f4v v) {
+#ifdef BDL_NT_STORE
+  __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
+#else
+  *reinterpret_cast<f4v*>(p) = v;
+#endif
+}
+
+__device__ __forceinline__ f4v ld4(const float* __restrict__ p, int64_t e, int64_t n) {
+  if (e + 4 <= n) return vload(p + e);
+  f4v v = {0.f, 0.f, 0.f, 0.f};
+  if (e + 0 < n) v.x = p[e + 0];
+  if (e + 1 < n) v.y = p[e + 1];
+  if (e + 2 < n) v.z = p[e + 2];
+  return v;
+}
+
+__device__ __forceinline__ void st4(float* __restrict__ p, int64_t e, int64_t n, f4v v) {
+  if (e + 4 <= n) {
+    vstore(p + e, v);
+    return;
+  }
+  if (e + 0 < n) p[e + 0] = v.x;
+  if (e + 1 < n) p[e + 1] = v.y;
+  if (e + 2 < n) p[e + 2] = v.z;
+}
+
+struct KArgs {
+  float* __restrict__ theta;
+  float* __restrict__ grad;
+  float* __restrict__ mom;
+  const float* __restrict__ prior_mean;
+  const float* __restrict__ noise;
+  float* __restrict__ mom1;
+  float* __restrict__ mom2;
+  const bdl_run* __restrict__ runs;
+  int32_t nruns;
+  int32_t flags;
+  int64_t n;
+  int64_t groups_per_block;
+  float lr0, lr1, ns0, ns1;
+  float one_minus_alpha, prior_sig, sigma2, n_data, mu, ca, cb;
+  uint64_t seed, chain, step;
+  const float* __restrict__ clip;  // (total_norm, coef) from the clip finalize, or null
+  // Adam-preconditioned SGHMC only (bdl_adam_step)
+  float* __restrict__ adam_m;
+  float* __restrict__ adam_v;
+  float* __restrict__ sgd_buf;
+  float b1, omb1, b2, omb2, bc1, bc2, aeps, two_alpha, nd, temp;
+  // scalar-divisor reciprocals for BDL_FLAG_RECIP_DIV (host-rounded fl32(1/s64))
+  float inv_s2, inv_nd, inv_ca, inv_cb, inv_temp, inv_bc1, inv_bc2;
+};
+
+// fl32(1/s64) from the caller, or 1/fl32(s) when it left the field 0
+inline float recip_or(float inv, float s) { return inv != 0.0f ? inv : 1.0f / s; }
+
+constexpr int32_t kFlagGradIsMom = 0x1000;  // internal: bdl_adam_args.grad_is_mom
+
+// Scalar division in the reference's rounding: torch CPU divides (x / s);
+// torch on a HIP device multiplies by the fp32 reciprocal (x * fl(1/s)).
+template <bool RECIP>
+__device__ __forceinline__ float sdiv(float x, float s, float inv_s) {
+  if constexpr (RECIP)
+    return x * inv_s;
+  else
+    return x / s;
+}
+
+// ---------------------------------------------------------------------------
+// Run table staged in LDS (dynamic, 16 B per run, sized per launch).  The fast
+// path reads the block-uniform attribute of its iteration from LDS, so the
+// wait for it is an lgkmcnt wait and never sits behind the data stream's
+// in-order vmcnt.
+// ---------------------------------------------------------------------------
+constexpr int kMaxRuns = 4096;  // 64 KiB of LDS
+
+extern __shared__ bdl_run s_runs[];
+
+__device__ __forceinline__ int64_t run_end(int r) { return s_runs[r].end; }
+__device__ __forceinline__ uint32_t run_attr(int r) { return s_runs[r].attr; }
+
+// First run whose end is > idx.
+__device__ __forceinline__ int find_run_lds(int nruns, int64_t idx) {
+  int lo = 0, hi = nruns - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (run_end(mid) <= idx)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+struct StepConst {
+  bool sgd_mom, sgd_mom_read, has_m2, grad_ready, clip;
+  float inv_s2, inv_nd, inv_ca, inv_cb, clip_coef;
+};
+
+// ---------------------------------------------------------------------------
+// Per-element update.  All arithmetic is separately rounded fp32 in exactly
+// the reference's op order (the file is compiled with -ffp-contract=off).
+// eta / ns are the element's lr and noise scale (its lr group), PRIOR whether
+// the Gaussian-prior term applies, GR = grad already formed (SGD step only).
+// ---------------------------------------------------------------------------
+template <int METHOD, int NOISE, bool RECIP, bool PRIOR, bool GR>
+__device__ __forceinline__ void update_core(const KArgs& a, const StepConst& c, float eta,
+                                            float ns, float& th, float& g, float& v, float th0,
+                                            float eps) {
+  if constexpr (GR) {
+    // the sampler gradient was formed (and possibly clipped) by a previous
+    // *_GRAD launch: only torch.optim.SGD's step remains
+    float stepv = g;
+    if (METHOD == BDL_SGLD && c.sgd_mom) {
+      v = (a.flags & BDL_FLAG_FIRST_STEP) ? g : (a.mu * v + g);
+      stepv = v;
+    }
+    th = fmaf(-eta, stepv, th);
+  } else if constexpr (METHOD == BDL_CSGHMC) {
+    // csghmc.py:759-762 — both branches are grad + prior_sig * theta (Q1)
+    const float t = a.prior_sig * th;
+    const float gU = g + t;
+    const float x = v * a.one_minus_alpha;  // :770 v*(1-a)
+    const float y = eta * gU;               //      lr*grad_U
+    float vn = x - y;
+    if constexpr (NOISE != BDL_NOISE_NONE) vn = vn + ns * eps;  // + noise (:765-770)
+    v = vn;                                 // :775
+    th = th + vn;                           // :778 p.data.add_(v)
+  } else if constexpr (METHOD == BDL_SGHMC || METHOD == BDL_SGHMC_GRAD) {
+    float gU = g;  // sghmc.py:494-497
+    if constexpr (PRIOR) {
+      const float d = th - th0;
+      const float e = sdiv<RECIP>(d, a.sigma2, c.inv_s2);
+      gU = g + sdiv<RECIP>(e, a.n_data, c.inv_nd);
+    }
+    const float s = v * a.one_minus_alpha + eta * gU;  // :504 (two products rounded)
+    const float vn = s + ns * eps;
+    const float gp = g + vn;  // :510 p.grad = p.grad + v
+    v = vn;
+    if constexpr (METHOD == BDL_SGHMC)
+      th = fmaf(-eta, gp, th);  // SGD(momentum=0): param.add_(grad, alpha=-lr)
+    else
+      g = gp;
+  } else {  // BDL_SGLD / BDL_SGLD_GRAD  (sgld.py:471-484)
+    const float nz = ns * eps;
+    float gp;
+    if constexpr (PRIOR) {
+      const float d = th - th0;
+      const float e = sdiv<RECIP>(d, a.sigma2, c.inv_s2);
+      const float f = sdiv<RECIP>(e, a.n_data, c.inv_nd);
+      gp = g + (f + nz);
+    } else {
+      gp = g + nz;
+    }
+    if constexpr (METHOD == BDL_SGLD) {
+      if (c.clip) gp = gp * c.clip_coef;  // clip_grad_norm_: grads.mul_(clip_coef_clamped)
+      float stepv = gp;
+      if (c.sgd_mom) {  // torch SGD momentum buffer
+        v = (a.flags & BDL_FLAG_FIRST_STEP) ? gp : (a.mu * v + gp);
+        stepv = v;
+      }
+      th = fmaf(-eta, stepv, th);
+    } else {
+      g = gp;
+    }
+  }
+}
+
+// Posterior moments on the updated theta (parameters_to_vector after step).
+template <int COLLECT, bool RECIP>
+__device__ __forceinline__ void collect_core(const KArgs& a, const StepConst& c, float th,
+                                             float& m1, float& m2) {
+  if constexpr (COLLECT == BDL_COLLECT_WELFORD_INIT) {
+    m1 = th;
+    m2 = 0.0f;
+  } else if constexpr (COLLECT == BDL_COLLECT_WELFORD) {
+    const float d = th - m1;
+    m1 = m1 + sdiv<RECIP>(d, a.ca, c.inv_ca);
+    const float d2 = th - m1;
+    m2 = m2 + d * d2;
+  } else if constexpr (COLLECT == BDL_COLLECT_MEAN_INIT) {
+    m1 = th;
+    m2 = th * th;
+  } else if constexpr (COLLECT == BDL_COLLECT_MEAN) {
+    m1 = sdiv<RECIP>(th + a.ca * m1, a.cb, c.inv_cb);
+    m2 = sdiv<RECIP>(th * th + a.ca * m2, a.cb, c.inv_cb);
+  }
+}
+
+// Per-kernel constants of a method / collect combination.
+template <int METHOD, int COLLECT>
+struct StepTraits {
+  static constexpr bool kReadPrior = (METHOD != BDL_CSGHMC);
+  static constexpr bool kMom =
+      (METHOD == BDL_CSGHMC || METHOD == BDL_SGHMC || METHOD == BDL_SGHMC_GRAD);
+  static constexpr bool kWriteTheta =
+      (METHOD == BDL_CSGHMC || METHOD == BDL_SGHMC || METHOD == BDL_SGLD);
+  static constexpr bool kWriteGrad = (METHOD == BDL_SGHMC_GRAD || METHOD == BDL_SGLD_GRAD);
+  static constexpr bool kCollect = (COLLECT != BDL_COLLECT_NONE);
+  static constexpr bool kReadMoments =
+      (COLLECT == BDL_COLLECT_WELFORD || COLLECT == BDL_COLLECT_MEAN);
+};
+
+// FAST PATH: a whole block-iteration (kBlock*UNROLL float4 groups) in range
+// and inside one non-skip run.  eta / ns are scalars, PRIOR / GR compile-time:
+// no branch inside, no bounds checks, every load issued before any arithmetic.
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL, bool PRIOR, bool GR>
+__device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, int64_t gb,
+                                           float eta, float ns) {
+  using T = StepTraits<METHOD, COLLECT>;
+  constexpr bool kPriorLoad = T::kReadPrior && PRIOR && !GR;
+  f4v th[UNROLL], g[UNROLL], v[UNROLL], t0[UNROLL], ep[UNROLL], m1[UNROLL], m2[UNROLL];
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+    v[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
+    th[u] = vload(a.theta + e);
+    g[u] = vload(a.grad + e);
+    if constexpr (T::kMom) v[u] = vload(a.mom + e);
+    if constexpr (METHOD == BDL_SGLD) {
+      if (c.sgd_mom_read) v[u] = vload(a.mom + e);
+    }
+    if constexpr (kPriorLoad) t0[u] = vload(a.prior_mean + e);
+    if constexpr (NOISE == BDL_NOISE_BUFFER && !GR) ep[u] = vload(a.noise + e);
+    if constexpr (T::kReadMoments) {
+      m1[u] = vload(a.mom1 + e);
+      if (c.has_m2) m2[u] = vload(a.mom2 + e);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    const int64_t e = gi * 4;
+    if constexpr (NOISE == BDL_NOISE_PHILOX && !GR)
+      ep[u] = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float xt = th[u][j], xg = g[u][j], xv = v[u][j], x1 = m1[u][j], x2 = m2[u][j];
+      update_core<METHOD, NOISE, RECIP, PRIOR, GR>(a, c, eta, ns, xt, xg, xv, t0[u][j], ep[u][j]);
+      collect_core<COLLECT, RECIP>(a, c, xt, x1, x2);
+      th[u][j] = xt;
+      g[u][j] = xg;
+      v[u][j] = xv;
+      m1[u][j] = x1;
+      m2[u][j] = x2;
+    }
+    if constexpr (T::kWriteTheta) vstore(a.theta + e, th[u]);
+    if constexpr (T::kWriteGrad) vstore(a.grad + e, g[u]);
+    if constexpr (T::kMom) vstore(a.mom + e, v[u]);
+    if constexpr (METHOD == BDL_SGLD) {
+      if (c.sgd_mom) vstore(a.mom + e, v[u]);
+    }
+    if constexpr (T::kCollect) {
+      vstore(a.mom1 + e, m1[u]);
+      if (c.has_m2) vstore(a.mom2 + e, m2[u]);
+    }
+  }
+}
+
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
+__device__ __forceinline__ void chunk_fast_dispatch(const KArgs& a, const StepConst& c,
+                                                    int64_t gb, uint32_t attr) {
+  const bool head = (attr & BDL_ATTR_HEAD) != 0;
+  const float eta = head ? a.lr1 : a.lr0;
+  const float ns = head ? a.ns1 : a.ns0;
+  if constexpr (METHOD == BDL_CSGHMC) {
+    chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(a, c, gb, eta, ns);
+  } else {
+    if constexpr (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) {
+      if (c.grad_ready) {
+        chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, true>(a, c, gb, eta, ns);
+        return;
+      }
+    }
+    if (attr & BDL_ATTR_PRIOR)
+      chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, true, false>(a, c, gb, eta, ns);
+    else
+      chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(a, c, gb, eta, ns);
+  }
+}
+
+// Element-wise update for the slow path: attribute-dependent branches allowed.
+template <int METHOD, int NOISE, int COLLECT, bool RECIP>
+__device__ __forceinline__ void update_elem(const KArgs& a, const StepConst& c, uint32_t attr,
+                                            float& th, float& g, float& v, float th0, float eps,
+                                            float& m1, float& m2) {
+  const bool head = (attr & BDL_ATTR_HEAD) != 0;
+  const float eta = head ? a.lr1 : a.lr0;
+  const float ns = head ? a.ns1 : a.ns0;
+  if (!(attr & BDL_ATTR_SKIP)) {
+    if ((METHOD == BDL_SGLD || METHOD == BDL_SGHMC) && c.grad_ready) {
+      if constexpr (METHOD == BDL_SGLD || METHOD == BDL_SGHMC)
+        update_core<METHOD, NOISE, RECIP, false, true>(a, c, eta, ns, th, g, v, th0, eps);
+    } else if (attr & BDL_ATTR_PRIOR) {
+      update_core<METHOD, NOISE, RECIP, true, false>(a, c, eta, ns, th, g, v, th0, eps);
+    } else {
+      update_core<METHOD, NOISE, RECIP, false, false>(a, c, eta, ns, th, g, v, th0, eps);
+    }
+  }
+  collect_core<COLLECT, RECIP>(a, c, th, m1, m2);
+}
+
+// SLOW PATH: an iteration that reaches the end of the vector / span, crosses a
+// run boundary or covers a skipped parameter.  Per-lane predicates, guarded
+// partial groups, a per-element run search (in LDS).  Taken for
+// O(#runs + #blocks) iterations per launch.
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
+__device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, int64_t gb,
+                                           int64_t gend) {
+  using T = StepTraits<METHOD, COLLECT>;
+  const int64_t n = a.n;
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    if (gi >= gend) continue;
+    const int64_t e = gi * 4;
+    const f4v z = {0.f, 0.f, 0.f, 0.f};
+    f4v th = ld4(a.theta, e, n), g = ld4(a.grad, e, n), v = z, t0 = z, ep = z, m1 = z, m2 = z;
+    if (T::kMom || (METHOD == BDL_SGLD && c.sgd_mom_read)) v = ld4(a.mom, e, n);
+    if (T::kReadPrior) t0 = ld4(a.prior_mean, e, n);
+    if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, n);
+    if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+    if (T::kReadMoments) {
+      m1 = ld4(a.mom1, e, n);
+      if (c.has_m2) m2 = ld4(a.mom2, e, n);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (e + j >= n) break;
+      const uint32_t at = run_attr(find_run_lds(a.nruns, e + j));
+      float xt = th[j], xg = g[j], xv = v[j], x1 = m1[j], x2 = m2[j];
+      update_elem<METHOD, NOISE, COLLECT, RECIP>(a, c, at, xt, xg, xv, t0[j], ep[j], x1, x2);
+      th[j] = xt;
+      g[j] = xg;
+      v[j] = xv;
+      m1[j] = x1;
+      m2[j] = x2;
+    }
+    if (T::kWriteTheta) st4(a.theta, e, n, th);
+    if (T::kWriteGrad) st4(a.grad, e, n, g);
+    if (T::kMom || (METHOD == BDL_SGLD && c.sgd_mom)) st4(a.mom, e, n, v);
+    if (T::kCollect) {
+      st4(a.mom1, e, n, m1);
+      if (c.has_m2) st4(a.mom2, e, n, m2);
+    }
+  }
+}
+
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
+__device__ __forceinline__ void step_body(const KArgs& a) {
+  StepConst c;
+  c.sgd_mom = (METHOD == BDL_SGLD) && (a.flags & BDL_FLAG_MOMENTUM);
+  c.sgd_mom_read = c.sgd_mom && !(a.flags & BDL_FLAG_FIRST_STEP);
+  c.has_m2 = (COLLECT != BDL_COLLECT_NONE) && (a.mom2 != nullptr);
+  c.grad_ready = (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) && (a.flags & BDL_FLAG_GRAD_READY);
+  c.clip = (METHOD == BDL_SGLD) && a.clip != nullptr;
+  c.clip_coef = c.clip ? a.clip[1] : 1.0f;
+  c.inv_s2 = a.inv_s2;
+  c.inv_nd = a.inv_nd;
+  c.inv_ca = a.inv_ca;
+  c.inv_cb = a.inv_cb;
+
+  const int64_t ngroups = (a.n + 3) >> 2;
+  const int64_t nfull = a.n >> 2;  // groups entirely inside [0, n)
+  // Two sweep orders: each block owns one contiguous span (groups_per_block >
+  // 0), or all blocks advance through the vector together (grid-stride,
+  // groups_per_block == 0).  Either way the block's iterations only move
+  // forward, so its (block-uniform) run cursor advances monotonically.
+  constexpr int64_t kIter = (int64_t)kBlock * UNROLL;
+  int64_t g0, g1, gstep;
+  if (a.groups_per_block > 0) {
+    g0 = (int64_t)blockIdx.x * a.groups_per_block;
+    g1 = min(g0 + a.groups_per_block, ngroups);
+    gstep = kIter;
+  } else {
+    g0 = (int64_t)blockIdx.x * kIter;
+    g1 = ngroups;
+    gstep = (int64_t)gridDim.x * kIter;
+  }
+
+  // stage the run table in LDS
+  for (int i = threadIdx.x; i < a.nruns; i += kBlock) s_runs[i] = a.runs[i];
+  __syncthreads();
+  if (g0 >= g1) return;
+
+  int r = find_run_lds(a.nruns, g0 * 4);
+  for (int64_t gb = g0; gb < g1; gb += gstep) {
+    while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
+    const int64_t gend = min(gb + kIter, g1);
+    const uint32_t attr = run_attr(r);
+    if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 &&
+        !(attr & BDL_ATTR_SKIP))
+      chunk_fast_dispatch<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, attr);
+    else
+      chunk_slow<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, gend);
+  }
+}
+
+template <int METHOD, int NOISE, int COLLECT, int UNROLL>
+__global__ __launch_bounds__(kBlock) void bdl_step_kernel(const KArgs a) {
+  if (a.flags & BDL_FLAG_RECIP_DIV)
+    step_body<METHOD, NOISE, COLLECT, true, UNROLL>(a);
+  else
+    step_body<METHOD, NOISE, COLLECT, false, UNROLL>(a);
+}
+
+// ---------------------------------------------------------------------------
+// Adam-preconditioned SGHMC (methods/adam_sghmc.py:500-553,
+// methods/adam_csghmc.py:812-860) + torch.optim.SGD step + running moments.
+// Same sweep as the SG-MCMC step (run table in LDS, branch-free fast path over
+// whole iterations inside one run, guarded slow path elsewhere); the element
+// update carries three more state vectors (v_mom in args.mom, Adam m and v) and
+// optionally the SGD buffer: 40 B/element, 48 with the buffer.
+// ---------------------------------------------------------------------------
+struct AdamConst {
+  bool sgd_mom, sgd_mom_read, has_m2, grad_is_mom;
+  float inv_s2, inv_nd, inv_temp, inv_bc1, inv_bc2, inv_ca, inv_cb;
+};
+
+template <int NOISE, bool RECIP, bool PRIOR, bool GRADONLY>
+__device__ __forceinline__ void adam_core(const KArgs& a, const AdamConst& c, float eta, float& th,
+                                          float& g, float& vm, float& m, float& v, float& buf,
+                                          float th0, float eps) {
+  const float gs = sdiv<RECIP>(g, a.temp, c.inv_temp);  // p.grad / temperature
+  float gU = gs;
+  if constexpr (PRIOR) {
+    const float d = th - th0;
+    const float e = sdiv<RECIP>(d, a.sigma2, c.inv_s2);
+    gU = gs + sdiv<RECIP>(e, a.n_data, c.inv_nd);
+  }
+  m = m * a.b1 + gU * a.omb1;            // beta1*m + (1-beta1)*grad_U
+  v = v * a.b2 + (gU * gU) * a.omb2;     // beta2*v + (1-beta2)*(grad_U*grad_U)
+  const float mh = sdiv<RECIP>(m, a.bc1, c.inv_bc1);
+  const float vh = sdiv<RECIP>(v, a.bc2, c.inv_bc2);
+  const float den = sqrtf(vh) + a.aeps;  // torch.sqrt(v_hat) + eps
+  const float pg = mh / den;             // precond_grad (tensor / tensor: true division)
+  const float pt = 1.0f / den;           // precond_term = 1.0 / (...) = reciprocal() * 1.0
+  float nz = 0.0f;
+  if constexpr (NOISE != BDL_NOISE_NONE) {
+    const float q = sdiv<RECIP>(pt * a.two_alpha, a.n_data, c.inv_nd);
+    nz = (sqrtf(q) * a.nd) * eps;        // nd*sqrt(2a*pt/N) * randn_like
+  }
+  vm = (vm * a.one_minus_alpha + pg * eta) + nz;
+  const float gp = c.grad_is_mom ? vm : g + vm;  // p.grad = v_mom (.clone()) | p.grad + v_mom
+  if constexpr (GRADONLY) {
+    g = gp;
+  } else {
+    float stepv = gp;
+    if (c.sgd_mom) {
+      buf = (a.flags & BDL_FLAG_FIRST_STEP) ? gp : (a.mu * buf + gp);
+      stepv = buf;
+    }
+    th = fmaf(-eta, stepv, th);  // SGD: param.add_(d_p, alpha=-lr)
+  }
+}
+
+template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, bool PRIOR, int U>
+__device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, int64_t gb,
+                                          float eta) {
+  constexpr bool kReadMoments = (COLLECT == BDL_COLLECT_MEAN);
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+  f4v th[U], g[U], vm[U], m[U], v[U], buf[U], t0[U], ep[U], m1[U], m2[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+    buf[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
+    th[u] = vload(a.theta + e);
+    g[u] = vload(a.grad + e);
+    vm[u] = vload(a.mom + e);
+    m[u] = vload(a.adam_m + e);
+    v[u] = vload(a.adam_v + e);
+    if (!GRADONLY && c.sgd_mom_read) buf[u] = vload(a.sgd_buf + e);
+    if constexpr (PRIOR) t0[u] = vload(a.prior_mean + e);
+    if constexpr (NOISE == BDL_NOISE_BUFFER) ep[u] = vload(a.noise + e);
+    if constexpr (kReadMoments) {
+      m1[u] = vload(a.mom1 + e);
+      if (c.has_m2) m2[u] = vload(a.mom2 + e);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    const int64_t e = gi * 4;
+    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+    StepConst cc;  // collect_core only reads inv_ca / inv_cb
+    cc.inv_ca = c.inv_ca;
+    cc.inv_cb = c.inv_cb;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float xt = th[u][j], xg = g[u][j], xvm = vm[u][j], xm = m[u][j], xv = v[u][j],
+            xb = buf[u][j], x1 = m1[u][j], x2 = m2[u][j];
+      adam_core<NOISE, RECIP, PRIOR, GRADONLY>(a, c, eta, xt, xg, xvm, xm, xv, xb, t0[u][j],
+                                               ep[u][j]);
+      collect_core<COLLECT, RECIP>(a, cc, xt, x1, x2);
+      th[u][j] = xt;
+      g[u][j] = xg;
+      vm[u][j] = xvm;
+      m[u][j] = xm;
+      v[u][j] = xv;
+      buf[u][j] = xb;
+      m1[u][j] = x1;
+      m2[u][j] = x2;
+    }
+    if constexpr (GRADONLY)
+      vstore(a.grad + e, g[u]);
+    else
+      vstore(a.theta + e, th[u]);
+    vstore(a.mom + e, vm[u]);
+    vstore(a.adam_m + e, m[u]);
+    vstore(a.adam_v + e, v[u]);
+    if (!GRADONLY && c.sgd_mom) vstore(a.sgd_buf + e, buf[u]);
+    if constexpr (COLLECT != BDL_COLLECT_NONE) {
+      vstore(a.mom1 + e, m1[u]);
+      if (c.has_m2) vstore(a.mom2 + e, m2[u]);
+    }
+  }
+}
+
+template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, int U>
+__device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, int64_t gb,
+                                          int64_t gend) {
+  const int64_t n = a.n;
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+  StepConst cc;
+  cc.inv_ca = c.inv_ca;
+  cc.inv_cb = c.inv_cb;
+  for (int u = 0; u < U; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    if (gi >= gend) continue;
+    const int64_t e = gi * 4;
+    f4v th = ld4(a.theta, e, n), g = ld4(a.grad, e, n), vm = ld4(a.mom, e, n);
+    f4v m = ld4(a.adam_m, e, n), v = ld4(a.adam_v, e, n), t0 = ld4(a.prior_mean, e, n);
+    f4v buf = z, ep = z, m1 = z, m2 = z;
+    if (!GRADONLY && c.sgd_mom_read) buf = ld4(a.sgd_buf, e, n);
+    if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, n);
+    if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+    if (COLLECT == BDL_COLLECT_MEAN) {
+      m1 = ld4(a.mom1, e, n);
+      if (c.has_m2) m2 = ld4(a.mom2, e, n);
+    }
+    for (int j = 0; j < 4; ++j) {
+      if (e + j >= n) break;
+      const uint32_t at = run_attr(find_run_lds(a.nruns, e + j));
+      float xt = th[j], xg = g[j], xvm = vm[j], xm = m[j], xv = v[j], xb = buf[j];
+      float x1 = m1[j], x2 = m2[j];
+      if (!(at & BDL_ATTR_SKIP)) {
+        const float eta = (at & BDL_ATTR_HEAD) ? a.lr1 : a.lr0;
+        if (at & BDL_ATTR_PRIOR)
+          adam_core<NOISE, RECIP, true, GRADONLY>(a, c, eta, xt, xg, xvm, xm, xv, xb, t0[j], ep[j]);
+        else
+          adam_core<NOISE, RECIP, false, GRADONLY>(a, c, eta, xt, xg, xvm, xm, xv, xb, t0[j], ep[j]);
+      }
+      collect_core<COLLECT, RECIP>(a, cc, xt, x1, x2);
+      th[j] = xt;
+      g[j] = xg;
+      vm[j] = xvm;
+      m[j] = xm;
+      v[j] = xv;
+      buf[j] = xb;
+      m1[j] = x1;
+      m2[j] = x2;
+    }
+    if (GRADONLY)
+      st4(a.grad, e, n, g);
+    else
+      st4(a.theta, e, n, th);
+    st4(a.mom, e, n, vm);
+    st4(a.adam_m, e, n, m);
+    st4(a.adam_v, e, n, v);
+    if (!GRADONLY && c.sgd_mom) st4(a.sgd_buf, e, n, buf);
+    if (COLLECT != BDL_COLLECT_NONE) {
+      st4(a.mom1, e, n, m1);
+      if (c.has_m2) st4(a.mom2, e, n, m2);
+    }
+  }
+}
+
+template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, int U>
+__device__ __forceinline__ void adam_body(const KArgs& a) {
+  AdamConst c;
+  c.sgd_mom = !GRADONLY && (a.flags & BDL_FLAG_MOMENTUM);
+  c.sgd_mom_read = c.sgd_mom && !(a.flags & BDL_FLAG_FIRST_STEP);
+  c.has_m2 = (COLLECT != BDL_COLLECT_NONE) && (a.mom2 != nullptr);
+  c.grad_is_mom = (a.flags & kFlagGradIsMom) != 0;
+  c.inv_s2 = a.inv_s2;
+  c.inv_nd = a.inv_nd;
+  c.inv_temp = a.inv_temp;
+  c.inv_bc1 = a.inv_bc1;
+  c.inv_bc2 = a.inv_bc2;
+  c.inv_ca = a.inv_ca;
+  c.inv_cb = a.inv_cb;
+  constexpr int64_t kIter = (int64_t)kBlock * U;
+  const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
+  for (int i = threadIdx.x; i < a.nruns; i += kBlock) s_runs[i] = a.runs[i];
+  __syncthreads();
+  int r = find_run_lds(a.nruns, (int64_t)blockIdx.x * kIter * 4);
+  for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {
+    while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
+    const int64_t gend = min(gb + kIter, ngroups);
+    const uint32_t attr = run_attr(r);
+    if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 && !(attr & BDL_ATTR_SKIP)) {
+      const float eta = (attr & BDL_ATTR_HEAD) ? a.lr1 : a.lr0;
+      if (attr & BDL_ATTR_PRIOR)
+        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, true, U>(a, c, gb, eta);
+      else
+        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, false, U>(a, c, gb, eta);
+    } else {
+      adam_slow<NOISE, COLLECT, RECIP, GRADONLY, U>(a, c, gb, gend);
+    }
+  }
+}
+
+template <int NOISE, int COLLECT, bool GRADONLY, int U>
+__global__ __launch_bounds__(kBlock) void bdl_adam_kernel(const KArgs a) {
+  if (a.flags & BDL_FLAG_RECIP_DIV)
+    adam_body<NOISE, COLLECT, true, GRADONLY, U>(a);
+  else
+    adam_body<NOISE, COLLECT, false, GRADONLY, U>(a);
+}
+
+// ---------------------------------------------------------------------------
+// Kernel selection: one function pointer per (method, noise, collect, unroll)
+// instance; each method's instances live in their own translation unit
+// (bdl_step_*.hip, bdl_adam.hip) so the library compiles in parallel.
+// ---------------------------------------------------------------------------
+using StepKernel = void (*)(const KArgs);
+
+template <int METHOD, int NOISE, int COLLECT>
+StepKernel pick_unroll(int unroll) {
+  // Every unroll depth for cSGHMC and for the noise-bearing SGHMC / SGLD
+  // production kernels; the *_GRAD and test-only noise-free variants use the
+  // default depth to keep build time down.
+  constexpr bool kAllDepths =
+      METHOD == BDL_CSGHMC ||
+      ((METHOD == BDL_SGLD || METHOD == BDL_SGHMC) && NOISE != BDL_NOISE_NONE);
+  if constexpr (!kAllDepths) {
+    (void)unroll;
+    return bdl_step_kernel<METHOD, NOISE, COLLECT, 2>;
+  } else {
+    switch (unroll) {
+      case 1:
+        return bdl_step_kernel<METHOD, NOISE, COLLECT, 1>;
+      case 4:
+        return bdl_step_kernel<METHOD, NOISE, COLLECT, 4>;
+      default:
+        return bdl_step_kernel<METHOD, NOISE, COLLECT, 2>;
+    }
+  }
+}
+
+template <int METHOD, int NOISE>
+StepKernel pick_collect(int collect, int unroll) {
+  switch (collect) {
+    case BDL_COLLECT_NONE:
+      return pick_unroll<METHOD, NOISE, BDL_COLLECT_NONE>(unroll);
+    case BDL_COLLECT_WELFORD_INIT:
+      return pick_unroll<METHOD, NOISE, BDL_COLLECT_WELFORD_INIT>(unroll);
+    case BDL_COLLECT_WELFORD:
+      return pick_unroll<METHOD, NOISE, BDL_COLLECT_WELFORD>(unroll);
+    case BDL_COLLECT_MEAN_INIT:
+      return pick_unroll<METHOD, NOISE, BDL_COLLECT_MEAN_INIT>(unroll);
+    case BDL_COLLECT_MEAN:
+      return pick_unroll<METHOD, NOISE, BDL_COLLECT_MEAN>(unroll);
+  }
+  return nullptr;
+}
+
+template <int METHOD>
+StepKernel pick_noise(int noise, int collect, int unroll) {
+  switch (noise) {
+    case BDL_NOISE_NONE:
+      return pick_collect<METHOD, BDL_NOISE_NONE>(collect, unroll);
+    case BDL_NOISE_BUFFER:
+      return pick_collect<METHOD, BDL_NOISE_BUFFER>(collect, unroll);
+    case BDL_NOISE_PHILOX:
+      return pick_collect<METHOD, BDL_NOISE_PHILOX>(collect, unroll);
+  }
+  return nullptr;
+}
+
+StepKernel pick_step_csghmc(int noise, int collect, int unroll);
+StepKernel pick_step_sghmc(int method, int noise, int collect, int unroll);
+StepKernel pick_step_sgld(int method, int noise, int collect, int unroll);
+StepKernel pick_adam(int noise, int collect, bool grad_only, int unroll);
+
+}  // namespace bdl

@@ -1,0 +1,10 @@
+// bdl_step_csghmc.hip — cSGHMC step kernel instances (methods/csghmc.py:747-778).
+#include "bdl_kernels.hpp"
+
+namespace bdl {
+
+StepKernel pick_step_csghmc(int noise, int collect, int unroll) {
+  return pick_noise<BDL_CSGHMC>(noise, collect, unroll);
+}
+
+}  // namespace bdl
