@@ -192,22 +192,10 @@ AUTOTUNE_CANDIDATES = ((2, 1, 1), (1, 4, 1), (3, 1, 1), (2, 4, 1), (1, 2, 1), (2
 _TUNED = {}
 
 
-def autotune(n, device=None, reps=6, candidates=None, method="csghmc"):
-    """Pick the fastest launch geometry for an n-element sweep on this device.
-
-    The update of every element is independent of the launch geometry (noise
-    is keyed by element index), so the choice changes speed only, never
-    results.  Times the method's production kernel (cSGHMC exploration; SGLD
-    + SGD momentum with Philox noise; Adam-SGHMC + SGD momentum) on scratch
-    buffers (freed afterwards) and installs the winner process-wide.  Returns
-    (config, {config: ms})."""
-    import numpy as np
-
+def _scratch_launcher(n, dev, method):
+    """A closure launching `method`'s production kernel over scratch buffers of
+    n elements (the buffers live as long as the closure)."""
     from .flat import FlatState
-    dev = torch.device(device) if device is not None else torch.device("cuda",
-                                                                        torch.cuda.current_device())
-    if candidates is None:
-        candidates = AUTOTUNE_CANDIDATES
     st = FlatState.from_segments([("w", (int(n),))], None, device=dev,
                                  need_prior=method != "csghmc")
     st.theta.zero_()
@@ -236,7 +224,29 @@ def autotune(n, device=None, reps=6, candidates=None, method="csghmc"):
         def launch():
             adam_step(st, L.ADAM_SGHMC, **kw)
     else:
-        raise ValueError(f"autotune: unknown method {method!r}")
+        raise ValueError(f"unknown method {method!r}")
+    return launch
+
+
+def _device(device):
+    return torch.device(device) if device is not None else torch.device(
+        "cuda", torch.cuda.current_device())
+
+
+def autotune(n, device=None, reps=6, candidates=None, method="csghmc"):
+    """Pick the fastest launch geometry for an n-element sweep on this device.
+
+    The update of every element is independent of the launch geometry (noise
+    is keyed by element index), so the choice changes speed only, never
+    results.  Times the method's production kernel (cSGHMC exploration; SGLD
+    + SGD momentum with Philox noise; Adam-SGHMC + SGD momentum) on scratch
+    buffers (freed afterwards) and installs the winner process-wide.  Returns
+    (config, {config: ms})."""
+    import numpy as np
+    dev = _device(device)
+    if candidates is None:
+        candidates = AUTOTUNE_CANDIDATES
+    launch = _scratch_launcher(n, dev, method)
     times = {}
     for cfg in candidates:
         set_launch_config(*cfg)
@@ -252,9 +262,29 @@ def autotune(n, device=None, reps=6, candidates=None, method="csghmc"):
         times[cfg] = float(np.median([a.elapsed_time(b) for a, b in ev]))
     best = min(times, key=times.get)
     set_launch_config(*best)
-    del st
+    del launch
     torch.cuda.empty_cache()
     return best, times
+
+
+def prewarm(n, device=None, method="csghmc", seconds=2.5):
+    """Run the method's kernel back to back on scratch buffers for `seconds`
+    (untimed setup before a measurement): the GPU's clocks ramp over the first
+    ~2-3 s of sustained load (tools/drift.py: 1.07 -> 1.04 ms per ViT-L/32
+    sweep), so a short measurement from idle would read the ramp, not the
+    steady state.  Returns the number of launches."""
+    import time
+    dev = _device(device)
+    launch = _scratch_launcher(n, dev, method)
+    t_end, k = time.perf_counter() + float(seconds), 0
+    while time.perf_counter() < t_end:
+        for _ in range(20):
+            launch()
+        k += 20
+        torch.cuda.synchronize(dev)
+    del launch
+    torch.cuda.empty_cache()
+    return k
 
 
 def autotune_once(n, device, method):

@@ -57,8 +57,38 @@ def parse():
     ap.add_argument("--grid-stride", type=int, default=-1)
     ap.add_argument("--no-autotune", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=10)
+    ap.add_argument("--prewarm-seconds", type=float, default=0.0,
+                    help="untimed back-to-back launches before the measurement (clock ramp)")
+    ap.add_argument("--event-stride", type=int, default=1,
+                    help="bracket every k-th timed launch with HIP events (1 = all)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
+
+
+class LaunchTimer:
+    """HIP events (torch.cuda.Event, on the stream the kernels run on) around
+    every `stride`-th timed launch and around the first launch of each kernel
+    kind; per-kind durations in ms."""
+
+    def __init__(self, stride=1):
+        self.stride, self.i, self.seen, self.recs = max(1, int(stride)), 0, set(), []
+
+    def begin(self, kind):
+        take = self.i % self.stride == 0 or kind not in self.seen
+        self.i += 1
+        if not take:
+            return None
+        self.seen.add(kind)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        self.recs.append((kind, ev))
+        return ev
+
+    def durations(self):
+        per = {}
+        for kind, (e0, e1) in self.recs:
+            per.setdefault(kind, []).append(e0.elapsed_time(e1))
+        return per
 
 
 def dist_setup():
@@ -156,6 +186,12 @@ def main():
     from bayesdll_amd.shapes import segments
 
     segs, readout = segments(a.backbone, a.num_classes)
+    # untimed: bring the GPU to its steady-state clocks, then tune the launch
+    tune_method = {"csghmc": "csghmc", "sgld": "sgld", "adam_sghmc": "adam"}[a.method]
+    n_all = sum(int(np.prod(s)) for _, s in segs)
+    prewarm = {"seconds": a.prewarm_seconds,
+               "launches": K.prewarm(n_all, local, tune_method, a.prewarm_seconds)
+               if a.prewarm_seconds > 0 else 0}
     tuned = None
     if a.blocks_per_cu or a.unroll or a.grid_stride >= 0:
         K.set_launch_config(a.blocks_per_cu, a.unroll, max(a.grid_stride, 0))
@@ -164,9 +200,7 @@ def main():
     elif not a.no_autotune:
         # untimed setup (like cudnn.benchmark): pick the launch geometry for
         # this device; results are identical under every geometry
-        best, tuned = K.autotune(sum(int(np.prod(s)) for _, s in segs), device=local,
-                                 method={"csghmc": "csghmc", "sgld": "sgld",
-                                         "adam_sghmc": "adam"}[a.method])
+        best, tuned = K.autotune(n_all, device=local, method=tune_method)
         launch = {"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
                   "autotuned": True,
                   "candidates_ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4) for c, t in tuned.items()},
@@ -200,7 +234,7 @@ def main():
         K.moments_update(st.theta, m1s[0], m2s[0], L.COLLECT_MEAN_INIT)
         spc[0] = 1
 
-    def sgld_step(k, ev=None):
+    def sgld_step(k, timer=None):
         """methods/sgld.py:193-250: Model + SGD(momentum 0.5) + running moments
         every `thin` iterations, fused."""
         first = k == 0
@@ -209,8 +243,7 @@ def main():
         lrs = (lr, lr_head)
         ns = [nd * np.sqrt(2 / (N * x)) for x in lrs]
         cnt = spc[0]
-        if ev is not None:
-            ev[0].record()
+        ev = timer.begin(kind) if timer is not None else None
         K.sgmcmc_step(st, L.SGLD, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_PHILOX,
                       prior_sig=prior_sig, sigma2=prior_sig ** 2, n_data=N, mu=mu,
                       first_step=first, momentum=True,
@@ -228,15 +261,14 @@ def main():
         adam_v = torch.zeros(n, dtype=torch.float32, device=dev)
         sgd_buf = torch.empty(n, dtype=torch.float32, device=dev)
 
-    def adam_step(k, ev=None):
+    def adam_step(k, timer=None):
         """methods/adam_sghmc.py:458-553 + SGD(momentum 0.5) (:60, :229) +
         running moments every `thin` iterations, fused."""
         first = k == 0
         collect = (k + 1) % a.thin == 0
         kind = "adam_first" if first else ("adam_collect" if collect else "adam")
         cnt = spc[0]
-        if ev is not None:
-            ev[0].record()
+        ev = timer.begin(kind) if timer is not None else None
         K.adam_step(st, L.ADAM_SGHMC, adam_m=adam_m, adam_v=adam_v, sgd_buf=sgd_buf, beta1=0.9,
                     beta2=0.999, eps=1e-8, t=k + 1, momentum_decay=alpha, nd=nd,
                     lrs=(lr, lr_head), noise_mode=L.NOISE_PHILOX, sigma2=prior_sig ** 2,
@@ -267,7 +299,7 @@ def main():
                 kind = "collect"
         return cur, ss, kind, spec
 
-    def step(k, ev=None):
+    def step(k, timer=None):
         cur, ss, kind, spec = plan(k)
         lrs = (cur, cur * (lr_head / lr))
         ns = [nd * np.sqrt(2 * alpha * x) / N for x in lrs]
@@ -275,8 +307,7 @@ def main():
         if spec is not None:
             ckind, c, ca, cnt = spec
             m1, m2 = m1s[c], m2s[c]
-        if ev is not None:
-            ev[0].record()
+        ev = timer.begin(kind) if timer is not None else None
         K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=ns,
                       noise_mode=L.NOISE_PHILOX if ss else L.NOISE_NONE,
                       one_minus_alpha=1 - alpha, prior_sig=prior_sig, collect=ckind, mom1=m1,
@@ -292,15 +323,14 @@ def main():
     for k in range(a.warmup):
         step(k)
     torch.cuda.synchronize()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(a.steps)]
+    timer = LaunchTimer(a.event_stride)
     kinds = []
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        kinds.append(step(a.warmup + i, events[i]))
+        kinds.append(step(a.warmup + i, timer))
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -333,14 +363,12 @@ def main():
                       "ms": round((time.perf_counter() - t1) / 20 * 1e3, 4),
                       "finite": bool(torch.isfinite(out_lp).all())}
 
-    per = {}
-    for kind, (e0, e1) in zip(kinds, events):
-        per.setdefault(kind, []).append(e0.elapsed_time(e1))
+    per = timer.durations()
     table = {}
     for kind, ms in per.items():
         avg = float(np.mean(ms))
         gbs = BYTES_PER_ELEM[kind] * n / (avg * 1e-3) / 1e9
-        table[kind] = {"launches": len(ms), "avg_ms": round(avg, 4),
+        table[kind] = {"launches": kinds.count(kind), "timed": len(ms), "avg_ms": round(avg, 4),
                        "p10_ms": round(float(np.percentile(ms, 10)), 4),
                        "p90_ms": round(float(np.percentile(ms, 90)), 4),
                        "bytes_per_elem": BYTES_PER_ELEM[kind], "gbs": round(gbs, 1)}
@@ -381,6 +409,7 @@ def main():
         "hbm_gbs": round(hbm_gbs * world, 1),
         "eval_collective": collective,
         "launch": launch,
+        "prewarm": prewarm,
         "kernels": table,
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),

@@ -545,3 +545,35 @@ def test_adam_step_philox_equals_buffer():
         outs.append((st.theta.clone(), st.mom.clone(), m, v))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def ref_sghmc(st, lrs, ns, alpha, sigma, N):
+    """methods/sghmc.py:482-510 + SGD(momentum 0) with torch ops on the device."""
+    th, v = st.theta.clone(), st.mom.clone()
+    for (o, k, a) in zip(st.offsets, st.numels, st.attrs):
+        h = 1 if a & 1 else 0
+        p, p0, g = th[o:o + k], st.prior[o:o + k], st.grad[o:o + k]
+        gU = g + (p - p0) / (sigma ** 2) / N if a & 2 else g
+        vn = v[o:o + k] * (1 - alpha) + lrs[h] * gU + ns[h] * st.noise[o:o + k]
+        v[o:o + k] = vn
+        p.add_(g + vn.clone(), alpha=-lrs[h])
+    return th, v
+
+
+def test_full_size_vit_sghmc_matches_torch():
+    """ViT-L/32, uninformative biases (~300 runs), recip rounding: the SGHMC
+    momentum is bit-exact vs torch ops on the same GPU, theta within 1 ulp
+    (torch's add_(alpha=-lr) may or may not contract to an FMA)."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.shapes import vit_l_32
+    segs, readout = vit_l_32()
+    st = _state(segs, readout, bias="uninformative", need_prior=True, need_noise=True, seed=4)
+    lrs, alpha, sigma, N, nd = (1e-4, 1e-2), 0.18, 1.0, 1840.0, 0.01
+    ns = [nd * np.sqrt(2 * alpha / (N * lr)) for lr in lrs]
+    th_ref, v_ref = ref_sghmc(st, lrs, ns, alpha, sigma, N)
+    K.sgmcmc_step(st, L.SGHMC, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_BUFFER,
+                  one_minus_alpha=1 - alpha, sigma2=sigma ** 2, n_data=N, div_mode="recip")
+    torch.cuda.synchronize()
+    assert torch.equal(st.mom, v_ref)
+    np.testing.assert_allclose(st.theta.cpu().numpy(), th_ref.cpu().numpy(), rtol=2e-7, atol=1e-12)
