@@ -82,7 +82,39 @@ __device__ __forceinline__ f4v vload(const float* p) {
 }
 
 __device__ __forceinline__ void vstore(float* p, f4v v) {
-#ifdef BDL_NT_STORE
+#if defined(BDL_STORE_POLICY)
+  // A/B experiments: explicit cache-policy bits (1: sc1, 2: nt sc1, 3: sc0 sc1,
+  // 4: the compiler's nontemporal store = "nt")
+#if BDL_STORE_POLICY == 4
+  __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
+#elif BDL_STORE_POLICY == 5
+  // "nt sc1" through the raw-buffer builtin (hipcc tracks it: waitcnts and
+  // hazards handled by the compiler).  Wave-uniform base = the first active
+  // lane's address; every lane's 32-bit offset from it is >= 0 because the
+  // data-stream addresses increase with the lane id.
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const uintptr_t base = ((uintptr_t)hi << 32) | lo;
+  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), rs, (int)(a - base), 0,
+                                         18 /* nt | sc1 */);
+#elif BDL_STORE_POLICY == 1
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+#elif BDL_STORE_POLICY == 2
+  asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+#else
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+#endif
+#elif defined(BDL_NT_STORE)
+  // production: the compiler's non-temporal store ("nt").  Store-policy A/B
+  // (`make storepolicy P=<n>`, alternating full bench runs): "nt sc1"
+  // (write-through) read 1.3 % faster on a first box (asm form, before its
+  // store-data hazard was fixed with s_nop) and 0.6 % slower on a second box
+  // (hazard-free asm form and buffer-builtin form alike) — no consistent
+  // gain, so the compiler-tracked store stays.
   __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
 #else
   *reinterpret_cast<f4v*>(p) = v;
