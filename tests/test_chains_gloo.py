@@ -1,8 +1,9 @@
-"""Multi-chain logic on CPU with torch.distributed gloo, world_size 2 (stands in
-for RCCL over xGMI: the same all_reduce / all_gather calls)."""
+"""Multi-chain logic on CPU with torch.distributed gloo, world_size 2 and 4
+(stands in for RCCL over xGMI: the same all_reduce / all_gather calls)."""
 import os
 import socket
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -34,8 +35,9 @@ def _worker(r, world, port, q):
         dist.destroy_process_group()
 
 
-def test_average_predictive_and_gather_two_chains():
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world", [2, 4])
+def test_average_predictive_and_gather_chains(world):
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
@@ -48,10 +50,10 @@ def test_average_predictive_and_gather_two_chains():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    want = torch.log((res[0][0].exp() + res[1][0].exp()) / 2)
+    want = torch.log(sum(res[r][0].exp() for r in range(world)) / world)
     for r in range(world):
         torch.testing.assert_close(res[r][1], want)
-        torch.testing.assert_close(res[r][3], torch.cat([res[0][2], res[1][2]], dim=2))
+        torch.testing.assert_close(res[r][3], torch.cat([res[k][2] for k in range(world)], dim=2))
         assert res[r][4] == r            # Philox chain id = rank
         assert res[r][5] == 42 + r       # per-chain seed
     # the averaged predictive is a proper distribution
