@@ -221,3 +221,32 @@ def sample_average_evaluate(runner, test_loader, mean, m2, var_mode, ratio):
 
 __all__ = ["PosteriorDraw", "chain_average_logprob", "evaluate_point_estimate", "save_logits",
            "gmm_weights", "mixture_evaluate", "sample_average_evaluate", "L"]
+
+
+def reinit_network(net):
+    """Cold restart (methods/adam_csghmc.py:102-117, methods/csghmc_fs.py:93-117):
+    fresh random weights per layer type — Xavier-uniform Linear, Kaiming-uniform
+    (fan_in, ReLU) Conv2d, zero biases, unit/zero BatchNorm affine, else the
+    module's own reset_parameters().  In place, so parameters that are views
+    into a sampler's flat theta stay bound to it."""
+    import torch.nn as nn
+
+    def init(m):
+        if isinstance(m, nn.Linear):
+            nn.init.xavier_uniform_(m.weight)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, nn.Conv2d):
+            nn.init.kaiming_uniform_(m.weight, mode="fan_in", nonlinearity="relu")
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, (nn.BatchNorm2d, nn.BatchNorm1d)):
+            if m.weight is not None:
+                nn.init.ones_(m.weight)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif hasattr(m, "reset_parameters"):
+            m.reset_parameters()
+
+    with torch.no_grad():
+        net.apply(init)

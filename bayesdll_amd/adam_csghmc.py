@@ -15,9 +15,6 @@ variance) and checkpoint format are csgld's, as in the reference.
 """
 from __future__ import annotations
 
-import torch
-import torch.nn as nn
-
 from .adam_sghmc import Model as _AdamModel
 from .csgld import Runner as _CSGLDRunner
 
@@ -71,28 +68,11 @@ class Runner(_CSGLDRunner):
             self._reinitialize_network_fresh()
 
     def _reinitialize_network_fresh(self):
-        """:102-117.  The parameters are views into the flat theta buffer, so
-        the in-place nn.init calls write straight into the chain state."""
-        def fresh_weight_init(m):
-            if isinstance(m, nn.Linear):
-                nn.init.xavier_uniform_(m.weight)
-                if m.bias is not None:
-                    nn.init.zeros_(m.bias)
-            elif isinstance(m, nn.Conv2d):
-                nn.init.kaiming_uniform_(m.weight, mode="fan_in", nonlinearity="relu")
-                if m.bias is not None:
-                    nn.init.zeros_(m.bias)
-            elif isinstance(m, (nn.BatchNorm2d, nn.BatchNorm1d)):
-                if m.weight is not None:
-                    nn.init.ones_(m.weight)
-                if m.bias is not None:
-                    nn.init.zeros_(m.bias)
-            elif hasattr(m, "reset_parameters"):
-                m.reset_parameters()
-
-        with torch.no_grad():
-            self.net.apply(fresh_weight_init)
-        self._state().check_bound()
+        """Cold restart: `_runner.reinit_network`, in place in the flat theta."""
+        from . import _runner as R
+        R.reinit_network(self.net)
+        if self.model.flat is not None:
+            self.model.flat.check_bound()
 
     def evaluate_simple(self, test_loader):
         """:544-576: plain forward pass of the current network."""

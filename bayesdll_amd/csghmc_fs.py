@@ -22,7 +22,6 @@ import pickle
 
 import numpy as np
 import torch
-import torch.nn as nn
 
 from . import _runner as R
 from .csghmc import Model  # noqa: F401  (methods/csghmc_fs.py's Model is csghmc's)
@@ -55,26 +54,9 @@ class Runner(_CSGHMCRunner):
         self.logger.info("All optimizer states (momentum, m, v, t) reset for new cycle.")
 
     def _reinitialize_network_fresh(self):
-        """:93-117, in place: parameters are views into the flat theta."""
-        def fresh_weight_init(m):
-            if isinstance(m, nn.Linear):
-                nn.init.xavier_uniform_(m.weight)
-                if m.bias is not None:
-                    nn.init.zeros_(m.bias)
-            elif isinstance(m, nn.Conv2d):
-                nn.init.kaiming_uniform_(m.weight, mode="fan_in", nonlinearity="relu")
-                if m.bias is not None:
-                    nn.init.zeros_(m.bias)
-            elif isinstance(m, (nn.BatchNorm2d, nn.BatchNorm1d)):
-                if m.weight is not None:
-                    nn.init.ones_(m.weight)
-                if m.bias is not None:
-                    nn.init.zeros_(m.bias)
-            elif hasattr(m, "reset_parameters"):
-                m.reset_parameters()
-
-        with torch.no_grad():
-            self.net.apply(fresh_weight_init)
+        """Cold restart: `_runner.reinit_network`, in place in the flat theta."""
+        from . import _runner as R
+        R.reinit_network(self.net)
         if self.model.flat is not None:
             self.model.flat.check_bound()
 

@@ -1,7 +1,6 @@
 """Which fp32 torch ops are correctly rounded on this device/CPU?  Compares
 torch results with IEEE round-to-nearest references (float64 computation
 rounded once to fp32 -- exact for sqrt/div/reciprocal of fp32 inputs)."""
-import numpy as np
 import torch
 
 
