@@ -247,20 +247,31 @@ def autotune(n, device=None, reps=6, candidates=None, method="csghmc"):
     if candidates is None:
         candidates = AUTOTUNE_CANDIDATES
     launch = _scratch_launcher(n, dev, method)
-    times = {}
-    for cfg in candidates:
-        set_launch_config(*cfg)
-        for _ in range(2):
-            launch()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(reps)]
-        for e0, e1 in ev:
-            e0.record()
-            launch()
-            e1.record()
-        torch.cuda.synchronize(dev)
-        times[cfg] = float(np.median([a.elapsed_time(b) for a, b in ev]))
-    best = min(times, key=times.get)
+
+    def measure(cfgs, k):
+        out = {}
+        for cfg in cfgs:
+            set_launch_config(*cfg)
+            for _ in range(2):
+                launch()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(k)]
+            for e0, e1 in ev:
+                e0.record()
+                launch()
+                e1.record()
+            torch.cuda.synchronize(dev)
+            out[cfg] = float(np.median([a.elapsed_time(b) for a, b in ev]))
+        return out
+
+    # round 1: every candidate; round 2: the three fastest again with twice the
+    # repetitions, averaged with round 1 (damps the +-1-2 % burst-to-burst noise)
+    times = measure(candidates, reps)
+    top = sorted(times, key=times.get)[:3]
+    again = measure(top, 2 * reps)
+    for cfg in top:
+        times[cfg] = 0.5 * (times[cfg] + again[cfg])
+    best = min(top, key=times.get)
     set_launch_config(*best)
     del launch
     torch.cuda.empty_cache()
