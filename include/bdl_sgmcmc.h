@@ -2,7 +2,8 @@
  * bdl_sgmcmc.h — C-ABI of the MI355X-native fused SG-MCMC parameter update.
  *
  * This is the drop-in boundary for the per-step update of the reference's
- * methods/{csghmc,sghmc,csgld,sgld}.py Runner/Model step loop.  The Python host
+ * methods/{csghmc,sghmc,csgld,sgld}.py Runner/Model step loop (and of its
+ * variants methods/{csghmc_fs,adam_sghmc,adam_csghmc}.py).  The Python host
  * package (bayesdll_amd) binds these symbols with ctypes; any other host
  * (C, C++, another FFI) can bind them the same way — no torch types cross
  * this boundary, only plain device pointers, sizes and scalars.
@@ -22,6 +23,10 @@
  *       methods/csghmc.py:327-345 (Welford), methods/sgld.py:239-246 and
  *       methods/sghmc.py:242-249 (running mean), methods/csgld.py:280-293
  *       (per-cycle running mean)
+ *   bdl_sgld_step_clipped replaces methods/csgld.py:248-253 with args.clip_grad
+ *     (Model.forward, torch.nn.utils.clip_grad_norm_, optimizer.step()).
+ *   bdl_adam_step replaces methods/adam_sghmc.py:500-553 (+ SGD step, :229)
+ *     and methods/adam_csghmc.py:812-860 (+ SGD step, :322).
  *   bdl_moments_update replaces the stand-alone moment updates
  *     (methods/sgld.py:95-102 burn-in seeding; the same formulas as above
  *     when the caller does not fuse them into the step).
@@ -279,7 +284,8 @@ int bdl_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t chain,
                       uint64_t step, void* hip_stream);
 
 /* Launch geometry override for tuning (0 = default): workgroups per CU, float4
- * groups in flight per lane (1, 2, 4; the cSGHMC kernel only), and the sweep
+ * groups in flight per lane (1, 2, 4: the production kernels of every method;
+ * *_GRAD and noise-free test variants keep 2), and the sweep
  * order (0 = one contiguous span per workgroup, 1 = grid-stride).  Returns the
  * previous value packed as (grid_stride << 24) | (blocks_per_cu << 8) | unroll.
  * Process-global, not thread-safe; for tuning and tests. */
