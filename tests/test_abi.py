@@ -185,3 +185,36 @@ def test_entry_points_validate_before_touching_the_device():
     a.mom1 = 0x9000
     assert h.bdl_adam_step(a, ad, None) == -3                       # Welford not an Adam collect
     assert b"bdl_adam_step" in h.bdl_last_error()
+
+
+def test_plain_c_host_links_and_calls_the_abi(tmp_path):
+    """A C host (no Python, no torch) compiles against include/bdl_sgmcmc.h,
+    links libbdl_sgmcmc.so and uses the host-only entry points — the same
+    boundary a cgo / JNI / N-API binding would use."""
+    from bayesdll_amd import _lib as L
+    src = r"""
+#include <stdio.h>
+#include "bdl_sgmcmc.h"
+int main(void) {
+  bdl_segment segs[3] = {{0, 10, BDL_ATTR_PRIOR, 0}, {10, 3, 0, 0},
+                         {13, 5, BDL_ATTR_PRIOR | BDL_ATTR_HEAD, 0}};
+  bdl_run runs[8];
+  int nr = bdl_build_runs(segs, 3, 20, runs, 8);
+  printf("version %d runs %d", bdl_version(), nr);
+  for (int i = 0; i < nr; ++i) printf(" %lld:%u", (long long)runs[i].end, runs[i].attr);
+  int rc = bdl_sgmcmc_step(0, 0);
+  printf(" rc %d msg %s\n", rc, bdl_last_error());
+  return 0;
+}
+"""
+    c = tmp_path / "host.c"
+    exe = tmp_path / "host"
+    c.write_text(src)
+    libdir = os.path.dirname(L.LIB_PATH)
+    subprocess.check_call(["gcc", "-std=c99", "-I", os.path.dirname(HEADER), str(c), "-o", str(exe),
+                           "-L", libdir, "-lbdl_sgmcmc", f"-Wl,-rpath,{libdir}",
+                           "-Wl,-rpath,/opt/rocm/lib"])
+    out = subprocess.check_output([str(exe)]).decode()
+    assert out.startswith(f"version {L.ABI_VERSION} runs 4")
+    assert " 10:2 13:0 18:3 20:4 " in out
+    assert "rc -1 msg bdl_sgmcmc_step: null args" in out
