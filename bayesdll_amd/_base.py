@@ -70,7 +70,8 @@ class FusedModelBase(nn.Module):
             self._state = FlatState(net, net0, readout_name=getattr(net, "readout_name", None),
                                     bias=getattr(self, "bias", "informative"),
                                     need_prior=self.need_prior, need_mom=self.need_mom,
-                                    need_noise=self.noise_mode != "philox")
+                                    need_noise=self.noise_mode != "philox",
+                                    placement=self.tune_method)
             self._state_net = net
             # launch geometry for this device and size (speed only: results
             # never depend on it)

@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--e2e-steps", type=int, default=10)
     ap.add_argument("--prewarm-seconds", type=float, default=0.0,
                     help="untimed back-to-back launches before the measurement (clock ramp)")
+    ap.add_argument("--no-placement", dest="placement", action="store_false",
+                    help="allocate the chain vectors without placement tuning")
     ap.add_argument("--event-stride", type=int, default=1,
                     help="bracket every k-th timed launch with HIP events (1 = all)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -210,7 +212,8 @@ def main():
     dev = torch.device("cuda", local)
     adam = a.method == "adam_sghmc"
     sgld = a.method == "sgld" or adam  # adam shares config 3's state/driver shape
-    st = FlatState.from_segments(segs, readout, device=dev, need_prior=sgld)
+    st = FlatState.from_segments(segs, readout, device=dev, need_prior=sgld,
+                                 placement=tune_method if a.placement else None)
     gen = torch.Generator(device=dev).manual_seed(42 + rank)
     if sgld:  # config 3: theta0 ~ N(0, 0.02^2) (pretrained stand-in), theta = theta0 + N(0, 1e-3^2)
         st.prior.normal_(0.0, 0.02, generator=gen)
@@ -410,6 +413,7 @@ def main():
         "eval_collective": collective,
         "launch": launch,
         "prewarm": prewarm,
+        "placement": st.placement_info,
         "kernels": table,
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),

@@ -577,3 +577,32 @@ def test_full_size_vit_sghmc_matches_torch():
     torch.cuda.synchronize()
     assert torch.equal(st.mom, v_ref)
     np.testing.assert_allclose(st.theta.cpu().numpy(), th_ref.cpu().numpy(), rtol=2e-7, atol=1e-12)
+
+
+def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
+    """flat.placed_vectors: candidate sets are timed and the fastest kept; the
+    update itself never depends on where the vectors live."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.flat import FlatState, PLACEMENT_MIN_ELEMS
+    segs = [("l0.weight", (PLACEMENT_MIN_ELEMS // 4 + 3,)), ("fc.weight", (1024,))]
+    outs = []
+    for placement in (None, "csghmc"):
+        st = FlatState.from_segments(segs, "fc", device=DEV, placement=placement)
+        if placement is None:
+            assert st.placement_info is None
+        else:
+            info = st.placement_info
+            assert len(info["candidates_ms"]) >= 2
+            assert info["candidates_ms"][info["chosen"]] == min(info["candidates_ms"])
+        g = torch.Generator(device=DEV).manual_seed(0)
+        st.theta.normal_(0, 0.02, generator=g)
+        st.grad.normal_(0, 1e-3, generator=g)
+        st.mom.zero_()
+        for k in range(3):
+            K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-3, 1e-2), noise_scale=(1e-3, 1e-3),
+                          noise_mode=L.NOISE_PHILOX, one_minus_alpha=0.9, prior_sig=1.0,
+                          seed=5, step=k)
+        torch.cuda.synchronize()
+        outs.append((st.theta.clone(), st.mom.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
