@@ -585,7 +585,7 @@ def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
     from bayesdll_amd.flat import FlatState, PLACEMENT_MIN_ELEMS
-    segs = [("l0.weight", (PLACEMENT_MIN_ELEMS // 4 + 3,)), ("fc.weight", (1024,))]
+    segs = [("l0.weight", (PLACEMENT_MIN_ELEMS + 3,)), ("fc.weight", (1024,))]
     outs = []
     for placement in (None, "csghmc"):
         st = FlatState.from_segments(segs, "fc", device=DEV, placement=placement)
