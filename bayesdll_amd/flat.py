@@ -79,8 +79,13 @@ def placed_vectors(n, device, names, method, candidates=None):
     keep the fastest set, free the rest.  Results never depend on placement.
     Returns ({name: tensor}, info)."""
     import os
-    k = int(os.environ.get("BDL_PLACEMENT_CANDIDATES", "4")) if candidates is None else candidates
+    k = int(os.environ.get("BDL_PLACEMENT_CANDIDATES", "6")) if candidates is None else candidates
     f32 = dict(dtype=torch.float32, device=device)
+    if method is not None and k > 1 and n >= PLACEMENT_MIN_ELEMS:
+        # the candidates live at the same time: keep them within a quarter of
+        # the free HBM
+        free, _ = torch.cuda.mem_get_info(device)
+        k = min(k, int(0.25 * free // (len(names) * n * 4)))
     if method is None or k <= 1 or n < PLACEMENT_MIN_ELEMS:
         return {nm: torch.empty(n, **f32) for nm in names}, None
     from types import SimpleNamespace
