@@ -50,6 +50,7 @@ class FusedModelBase(nn.Module):
     need_prior = False
     need_mom = True
     tune_method = "sgld"  # which production kernel autotune_once times for this sampler
+    extra_vectors = ()    # further per-element state placed with the chain (FlatState.extra)
 
     def __init__(self):
         super().__init__()
@@ -71,7 +72,7 @@ class FusedModelBase(nn.Module):
                                     bias=getattr(self, "bias", "informative"),
                                     need_prior=self.need_prior, need_mom=self.need_mom,
                                     need_noise=self.noise_mode != "philox",
-                                    placement=self.tune_method)
+                                    placement=self.tune_method, extra=self.extra_vectors)
             self._state_net = net
             # launch geometry for this device and size (speed only: results
             # never depend on it)

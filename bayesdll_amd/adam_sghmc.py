@@ -61,6 +61,7 @@ class Model(FusedModelBase):
     need_prior = True
     need_mom = True   # v_mom (the reference's momentum_buffer)
     tune_method = "adam"
+    extra_vectors = ("adam_m", "adam_v", "sgd_buf")  # placed with theta / grad / v_mom
     grad_is_mom = False
 
     def __init__(self, ND, prior_sig=1.0, bias="informative", momentum_decay=0.05, beta1=0.9,
@@ -81,12 +82,17 @@ class Model(FusedModelBase):
     # ------------------------------------------------------------ state
     def adam_buffers(self, st):
         if self._adam is None or self._adam[0] is not st:
-            self._adam = (st, torch.zeros_like(st.theta), torch.zeros_like(st.theta))
+            ex = getattr(st, "extra", {})
+            m = ex["adam_m"] if "adam_m" in ex else torch.zeros_like(st.theta)
+            v = ex["adam_v"] if "adam_v" in ex else torch.zeros_like(st.theta)
+            self._adam = (st, m, v)
         return self._adam[1], self._adam[2]
 
     def ensure_sgd_buffer(self):
         if self.sgd_buffer is None:
-            self.sgd_buffer = torch.zeros_like(self._state.theta)
+            ex = getattr(self._state, "extra", {})
+            self.sgd_buffer = ex["sgd_buf"] if "sgd_buf" in ex else \
+                torch.zeros_like(self._state.theta)
         return self.sgd_buffer
 
     def _views(self, flat):

@@ -98,7 +98,14 @@ def placed_vectors(n, device, names, method, candidates=None):
         st = SimpleNamespace(theta=vs["theta"], grad=vs["grad"], mom=vs.get("mom"),
                              prior=vs.get("prior"), noise=None, runs=runs, nruns=1, n=n,
                              device=device)
-        if method == "csghmc":
+        if method == "adam" and "adam_m" in vs:
+            def launch():
+                K.adam_step(st, L.ADAM_SGHMC, adam_m=vs["adam_m"], adam_v=vs["adam_v"],
+                            sgd_buf=vs.get("sgd_buf"), beta1=0.9, beta2=0.999, eps=1e-8, t=3,
+                            momentum_decay=0.1, nd=0.01, lrs=(1e-4, 1e-4),
+                            noise_mode=L.NOISE_PHILOX, sigma2=1.0, n_data=1e6, mu=0.5,
+                            momentum="sgd_buf" in vs)
+        elif method == "csghmc":
             def launch():
                 K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-4, 1e-4), noise_scale=(0.0, 0.0),
                               noise_mode=L.NOISE_NONE, one_minus_alpha=0.9, prior_sig=1.0)
@@ -131,7 +138,8 @@ class FlatState:
     """Flat buffers for one chain, bound to `net`'s parameters and grads."""
 
     def __init__(self, net, net0=None, *, readout_name=None, bias="informative",
-                 need_prior=False, need_mom=True, need_noise=False, placement=None):
+                 need_prior=False, need_mom=True, need_noise=False, placement=None,
+                 extra=()):
         named = list(net.named_parameters())
         if not named:
             raise ValueError("bayesdll_amd: the network has no parameters")
@@ -154,8 +162,12 @@ class FlatState:
 
         # the swept vectors, placed (see placed_vectors) when `placement` names
         # the sampler's kernel family
-        names_ = ["theta", "grad"] + (["mom"] if need_mom else []) + (["prior"] if need_prior else [])
+        names_ = ["theta", "grad"] + (["mom"] if need_mom else []) + \
+            (["prior"] if need_prior else []) + list(extra)
         vecs, self.placement_info = placed_vectors(self.n, dev, names_, placement)
+        # further per-element state of the sampler (e.g. Adam's m, v and the
+        # SGD buffer), placed together with the swept vectors, zeroed
+        self.extra = {nm: vecs[nm].zero_() for nm in extra}
         # theta: copy then rebind every parameter as a view (same storage order
         # as nn.utils.parameters_to_vector)
         self.theta = vecs["theta"]
@@ -202,7 +214,7 @@ class FlatState:
     @classmethod
     def from_segments(cls, segments, readout_name, *, bias="informative", device="cuda",
                       need_prior=False, need_mom=True, need_noise=False, init=None,
-                      placement=None):
+                      placement=None, extra=()):
         """Flat chain state for a segment table alone (no nn.Module): the
         benchmark and kernel tests use it with synthetic vectors."""
         self = cls.__new__(cls)
@@ -219,9 +231,10 @@ class FlatState:
         self._grad_ptrs = []
         f32 = dict(dtype=torch.float32, device=self.device)
         names_ = (["theta"] if init is None else []) + ["grad"] + (["mom"] if need_mom else []) \
-            + (["prior"] if need_prior else [])
+            + (["prior"] if need_prior else []) + list(extra)
         vecs, self.placement_info = placed_vectors(
             self.n, self.device, names_, placement if init is None else None)
+        self.extra = {nm: vecs[nm].zero_() for nm in extra}
         self.theta = vecs["theta"] if init is None else init
         self.grad = vecs["grad"].zero_()
         self.mom = vecs["mom"].zero_() if need_mom else None

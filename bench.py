@@ -213,7 +213,8 @@ def main():
     adam = a.method == "adam_sghmc"
     sgld = a.method == "sgld" or adam  # adam shares config 3's state/driver shape
     st = FlatState.from_segments(segs, readout, device=dev, need_prior=sgld,
-                                 placement=tune_method if a.placement else None)
+                                 placement=tune_method if a.placement else None,
+                                 extra=("adam_m", "adam_v", "sgd_buf") if adam else ())
     gen = torch.Generator(device=dev).manual_seed(42 + rank)
     if sgld:  # config 3: theta0 ~ N(0, 0.02^2) (pretrained stand-in), theta = theta0 + N(0, 1e-3^2)
         st.prior.normal_(0.0, 0.02, generator=gen)
@@ -260,9 +261,7 @@ def main():
         return kind
 
     if adam:
-        adam_m = torch.zeros(n, dtype=torch.float32, device=dev)
-        adam_v = torch.zeros(n, dtype=torch.float32, device=dev)
-        sgd_buf = torch.empty(n, dtype=torch.float32, device=dev)
+        adam_m, adam_v, sgd_buf = st.extra["adam_m"], st.extra["adam_v"], st.extra["sgd_buf"]
 
     def adam_step(k, timer=None):
         """methods/adam_sghmc.py:458-553 + SGD(momentum 0.5) (:60, :229) +
