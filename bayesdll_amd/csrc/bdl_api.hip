@@ -6,21 +6,27 @@
 //   cSGHMC  methods/csghmc.py:747-778  (+ Welford collect :327-345)
 //   SGHMC   methods/sghmc.py:482-510   (+ SGD momentum 0, :229; moments :242-249)
 //   SGLD    methods/sgld.py:469-484    (+ SGD momentum mu, :226; moments :239-246)
-//   cSGLD   methods/csgld.py:665-680   (+ SGD, :253; per-cycle moments :280-293)
+//   cSGLD   methods/csgld.py:665-680   (+ SGD, :253; per-cycle moments :280-293;
+//           clip_grad_norm_ :250-251 through bdl_sgld_step_clipped)
+//   Adam-SGHMC  methods/adam_sghmc.py:500-553, methods/adam_csghmc.py:812-860
 //
 // Design:
-//   * elementwise, HBM-bound: no LDS on the data stream, no MFMA; 16-B (dwordx4)
-//     loads/stores per lane, several independent float4 groups in flight per
-//     lane, each workgroup sweeps one contiguous span of the vector.
+//   * elementwise, HBM-bound: no MFMA, no LDS on the data stream; 16-B
+//     (dwordx4) non-temporal loads/stores per lane, 1/2/4 independent float4
+//     groups in flight per lane, grid-stride sweep; workgroups per CU and
+//     depth autotuned per method (kernels.autotune).
 //   * per-element attributes (lr group, prior on/off, skip) come from a tiny
-//     sorted run table; a block finds its first run with a block-uniform
-//     (scalar) binary search and each lane advances a cursor monotonically.
+//     sorted run table staged in LDS; the block-uniform run cursor advances
+//     monotonically, and an iteration wholly inside one run takes the
+//     branch-free fast path.
 //   * noise: either read from a buffer (torch-RNG parity mode) or generated in
 //     registers by counter-based Philox4x32-10 keyed by (seed, chain, step,
 //     element/4) + Box-Muller on v_log/v_sin/v_cos — no extra HBM traffic.
 //   * every floating-point op is rounded separately in the reference's order
 //     (compiled with -ffp-contract=off); SGD's add(alpha=-lr) is an explicit
-//     fmaf, as torch's CPU kernel computes it.
+//     fmaf, as torch's CPU kernel computes it; tensor / Python-scalar
+//     divisions follow torch CPU (x / s) or torch on the device (x * fl32(1/s),
+//     reciprocal from the host's float64) per BDL_FLAG_RECIP_DIV.
 //
 // Files: bdl_kernels.hpp (device code shared by the kernel families),
 // bdl_step_{csghmc,sghmc,sgld}.hip and bdl_adam.hip (kernel instances per
@@ -38,11 +44,10 @@ int fail(int code, const char* msg) {
   return code;
 }
 
-// Tunables (bdl_set_launch_config).  blocks_per_cu * 256 CUs workgroups, each
-// lane keeps kUnroll float4 groups in flight per iteration.
-// Defaults from the gfx950 sweep (tools/sweep.py, profiles/round1/kernel_v1/sweep_*.log):
-// grid-stride with 2 workgroups/CU and 1 float4 group in flight per lane,
-// non-temporal 16-B loads and stores, measured best on every kernel kind.
+// Tunables (bdl_set_launch_config).  blocks_per_cu * #CUs workgroups, each
+// lane keeps `unroll` float4 groups in flight per iteration.  Defaults (2
+// workgroups/CU, depth 1, grid-stride) from the gfx950 sweep (tools/sweep.py,
+// profiles/round1/kernel_v1/sweep_*.log); the Python side autotunes per method.
 int g_blocks_per_cu = 2;
 int g_unroll = 1;
 int g_grid_stride = 1;  // 0: one contiguous span per block; 1: grid-stride sweep
