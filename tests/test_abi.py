@@ -218,3 +218,13 @@ int main(void) {
     assert out.startswith(f"version {L.ABI_VERSION} runs 4")
     assert " 10:2 13:0 18:3 20:4 " in out
     assert "rc -1 msg bdl_sgmcmc_step: null args" in out
+
+
+def test_missing_library_fails_loudly():
+    """No CPU fallback: without the built library the product raises."""
+    code = ("import bayesdll_amd._lib as L\n"
+            "try:\n    L.lib()\nexcept RuntimeError as e:\n    print('raised', e)\n")
+    env = dict(os.environ, BDL_SGMCMC_LIB="/nonexistent/libbdl_sgmcmc.so")
+    out = subprocess.run(["python", "-c", code], env=env, capture_output=True, text=True,
+                         cwd=os.path.dirname(HEADER) + "/..", timeout=300)
+    assert "raised" in out.stdout and "libbdl_sgmcmc" in out.stdout, out.stdout + out.stderr
