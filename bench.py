@@ -364,6 +364,23 @@ def main():
                       "backend": dist.get_backend(),
                       "ms": round((time.perf_counter() - t1) / 20 * 1e3, 4),
                       "finite": bool(torch.isfinite(out_lp).all())}
+        if dist.get_backend() != "gloo":
+            # the optional cross-chain pooled posterior mean: one full-vector
+            # all-reduce (1.2 GB for ViT-L/32) over RCCL / xGMI
+            chains.pool_moments(st.mom, None, count=1.0)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t2 = time.perf_counter()
+            for _ in range(3):
+                pooled, _ = chains.pool_moments(st.mom, None, count=1.0)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t2) / 3
+            nbytes = st.mom.numel() * 4
+            collective["pool_moments"] = {
+                "bytes": nbytes, "ms": round(dt * 1e3, 3),
+                "algbw_GBs": round(nbytes / dt / 1e9, 1),
+                "busbw_GBs": round(2 * (world - 1) / world * nbytes / dt / 1e9, 1)}
+            del pooled
 
     per = timer.durations()
     table = {}

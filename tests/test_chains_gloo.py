@@ -30,7 +30,10 @@ def _worker(r, world, port, q):
         avg = chains.average_predictive(logp)
         la = torch.randn(8, 5, 3, generator=g)
         gathered = chains.gather_logits(la)
-        q.put((r, logp, avg, la, gathered, default_chain(), chains.chain_seed(42)))
+        m1, m2 = torch.randn(1000, generator=g), torch.rand(1000, generator=g)
+        p1, p2 = chains.pool_moments(m1, m2, count=r + 1)
+        q.put((r, logp, avg, la, gathered, default_chain(), chains.chain_seed(42),
+               (m1, m2, p1, p2)))
     finally:
         dist.destroy_process_group()
 
@@ -45,8 +48,8 @@ def test_average_predictive_and_gather_chains(world):
         p.start()
     res = {}
     for _ in range(world):
-        r, logp, avg, la, gathered, chain, seed = q.get(timeout=120)
-        res[r] = (logp, avg, la, gathered, chain, seed)
+        r, logp, avg, la, gathered, chain, seed, mom = q.get(timeout=120)
+        res[r] = (logp, avg, la, gathered, chain, seed, mom)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -56,6 +59,13 @@ def test_average_predictive_and_gather_chains(world):
         torch.testing.assert_close(res[r][3], torch.cat([res[k][2] for k in range(world)], dim=2))
         assert res[r][4] == r            # Philox chain id = rank
         assert res[r][5] == 42 + r       # per-chain seed
+    # pooled moments: count-weighted average of the chains' moments
+    cnt = [r + 1 for r in range(world)]
+    want1 = sum(c * res[r][6][0].double() for r, c in enumerate(cnt)) / sum(cnt)
+    want2 = sum(c * res[r][6][1].double() for r, c in enumerate(cnt)) / sum(cnt)
+    for r in range(world):
+        torch.testing.assert_close(res[r][6][2].double(), want1, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(res[r][6][3].double(), want2, rtol=1e-6, atol=1e-6)
     # the averaged predictive is a proper distribution
     torch.testing.assert_close(want.exp().sum(1), torch.ones(8))
 
