@@ -606,3 +606,35 @@ def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
         torch.cuda.synchronize()
         outs.append((st.theta.clone(), st.mom.clone()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_full_size_vit_csghmc_sample_and_welford_collect_bitexact():
+    """The headline schedule's sample steps at full ViT-L/32 size: Philox noise
+    + Welford first sample (m1 = theta, M2 = 0) then a Welford update with the
+    reference's doubled count (Q2: n = 3 for the second sample), against
+    torch ops on the device fed the same Philox draws — bit-exact."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.shapes import vit_l_32
+    segs, readout = vit_l_32()
+    st = _state(segs, readout, seed=21)
+    st.noise = torch.empty_like(st.theta)
+    m1, m2 = torch.empty_like(st.theta), torch.empty_like(st.theta)
+    lrs, alpha, psig, N, nd = (1e-4, 1e-2), 0.18, 1.0, 1840.0, 0.01
+    ns = [nd * np.sqrt(2 * alpha * lr) / N for lr in lrs]
+    r1 = r2 = None
+    for k, (collect, n_) in enumerate(((L.COLLECT_WELFORD_INIT, 1.0), (L.COLLECT_WELFORD, 3.0))):
+        st.noise.copy_(K.philox_normal(st.n, 42, 0, 100 + k))
+        th_ref, v_ref = ref_csghmc(st, lrs, ns, alpha, psig, True)
+        if collect == L.COLLECT_WELFORD_INIT:
+            r1, r2 = th_ref.clone(), torch.zeros_like(th_ref)
+        else:
+            d = th_ref - r1
+            r1 = r1 + d / n_
+            r2 = r2 + d * (th_ref - r1)
+        K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_PHILOX,
+                      one_minus_alpha=1 - alpha, prior_sig=psig, collect=collect, mom1=m1,
+                      mom2=m2, collect_a=n_, seed=42, chain=0, step=100 + k, div_mode="recip")
+        torch.cuda.synchronize()
+        assert torch.equal(st.theta, th_ref) and torch.equal(st.mom, v_ref)
+        assert torch.equal(m1, r1) and torch.equal(m2, r2)
