@@ -250,3 +250,38 @@ def reinit_network(net):
 
     with torch.no_grad():
         net.apply(init)
+
+
+def resume_state(model, st, **counters):
+    """What an exact continuation of a chain needs beyond the reference's
+    checkpoint keys: the momentum / SGD buffer, the sampler's step counter
+    (the Philox noise key), host counters and the torch RNG states (the
+    "torch" noise mode draws from them)."""
+    out = {"mom": None if st.mom is None else st.mom.detach().clone(),
+           "step_count": int(model.step_count), "seed": int(model.seed),
+           "chain": int(model.chain),
+           "rng_cpu": torch.get_rng_state()}
+    if torch.cuda.is_available():
+        out["rng_cuda"] = torch.cuda.get_rng_state(st.device)
+    out.update(counters)
+    return out
+
+
+def restore_resume_state(model, st, ckpt):
+    """Inverse of resume_state (plus theta from the checkpoint's last_theta),
+    in place so the parameter and gradient views stay bound."""
+    rs = ckpt.get("resume")
+    if rs is None:
+        raise RuntimeError("checkpoint has no resume state (save it with args.resume_state=True)")
+    with torch.no_grad():
+        st.theta.copy_(ckpt["last_theta"].reshape(-1).to(st.theta.device))
+        if rs.get("mom") is not None and st.mom is not None:
+            st.mom.copy_(rs["mom"].to(st.mom.device))
+    model.step_count = int(rs["step_count"])
+    model.seed = int(rs["seed"])
+    model.chain = int(rs["chain"])
+    torch.set_rng_state(rs["rng_cpu"].cpu())
+    if "rng_cuda" in rs and torch.cuda.is_available():
+        torch.cuda.set_rng_state(rs["rng_cuda"].cpu(), st.device)
+    return {k: v for k, v in rs.items()
+            if k not in ("mom", "step_count", "seed", "chain", "rng_cpu", "rng_cuda")}

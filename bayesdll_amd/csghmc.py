@@ -87,7 +87,9 @@ class Runner:
         self.cycle_states = {}
 
     # ------------------------------------------------------------------ train
-    def train(self, train_loader, val_loader, test_loader):
+    def train(self, train_loader, val_loader, test_loader, start_epoch=0):
+        """methods/csghmc.py:87-209; start_epoch > 0 continues a chain restored
+        with load_ckpt(..., resume=True)."""
         args, logger = self.args, self.logger
         logger.info("Start training with Cyclical SGHMC (fused MI355X kernel)...")
         losses_train = np.zeros(args.epochs)
@@ -98,7 +100,7 @@ class Runner:
         errors_test = np.zeros(args.epochs)
         best_loss = np.inf
         tic0 = time.time()
-        for ep in range(args.epochs):
+        for ep in range(start_epoch, args.epochs):
             self.cyclical_scheduler.current_epoch = ep
             tic = time.time()
             losses_train[ep], errors_train[ep], cycle_updated = self.train_one_epoch(train_loader)
@@ -234,27 +236,41 @@ class Runner:
 
     def save_ckpt(self, epoch):
         """methods/csghmc.py:530-549 — same file name and keys; the flat theta
-        buffer IS parameters_to_vector(net.parameters())."""
+        buffer IS parameters_to_vector(net.parameters()).  With
+        args.resume_state (not in the reference, whose resume is inexact: it
+        saves no momentum) a "resume" entry adds what an exact
+        continuation needs: momentum, the sampler's step counter (the Philox
+        key), samples_collected and the torch RNG states."""
         fname = os.path.join(self.args.log_dir, f"{self.current_cycle}_ckpt.pt")
         st = self.model.state_for(self.net)
-        torch.save({"last_theta": st.theta.detach().clone(),
-                    "cycle_theta_mom1": self.cycle_theta_mom1,
-                    "cycle_theta_mom2": self.cycle_theta_mom2,
-                    "cycle_likelihoods": self.cycle_likelihoods,
-                    "cycle_states": self.cycle_states,
-                    "epoch": epoch,
-                    "current_cycle": self.current_cycle,
-                    "samples_per_cycle": self.samples_per_cycle}, fname)
+        ck = {"last_theta": st.theta.detach().clone(),
+              "cycle_theta_mom1": self.cycle_theta_mom1,
+              "cycle_theta_mom2": self.cycle_theta_mom2,
+              "cycle_likelihoods": self.cycle_likelihoods,
+              "cycle_states": self.cycle_states,
+              "epoch": epoch,
+              "current_cycle": self.current_cycle,
+              "samples_per_cycle": self.samples_per_cycle}
+        if getattr(self.args, "resume_state", False):
+            ck["resume"] = R.resume_state(self.model, st, samples_collected=self.samples_collected)
+        torch.save(ck, fname)
         return fname
 
-    def load_ckpt(self, ckpt_path):
-        """methods/csghmc.py:552-566 (same keys restored)."""
+    def load_ckpt(self, ckpt_path, resume=False):
+        """methods/csghmc.py:552-566 (same keys restored).  resume=True (with a
+        checkpoint saved under args.resume_state) also restores theta, the
+        momentum, the step counter and RNG states, so that
+        `train(..., start_epoch=epoch + 1)` continues the chain exactly."""
         ckpt = R.load_checkpoint(ckpt_path, self.args.device)
         self.cycle_theta_mom1 = ckpt.get("cycle_theta_mom1", {})
         self.cycle_theta_mom2 = ckpt.get("cycle_theta_mom2", {})
         self.cycle_likelihoods = ckpt.get("cycle_likelihoods", {})
         self.current_cycle = ckpt.get("current_cycle", 0)
         self.samples_per_cycle = ckpt.get("samples_per_cycle", {})
+        if resume:
+            st = self.model.state_for(self.net)
+            extra = R.restore_resume_state(self.model, st, ckpt)
+            self.samples_collected = extra.get("samples_collected", self.samples_collected)
         return ckpt["epoch"]
 
     def full_batch_likelihoods(self, train_loader):

@@ -339,3 +339,50 @@ def test_variant_runners_train_end_to_end(method, tmp_path):
                 "bma_evaluation_results.pkl", "logits_test_bma.pkl"} <= files
     else:
         assert runner.model.t == 0  # reset at the last cycle end
+
+
+def test_csghmc_exact_resume_from_checkpoint(tmp_path):
+    """args.resume_state: a chain restored from the cycle-1 checkpoint and
+    continued with train(start_epoch=2) lands bit-for-bit where the
+    uninterrupted run does (Philox noise keyed by the restored step counter)."""
+    import os
+    import bayesdll_amd.csghmc as csghmc
+    dev = "cuda"
+    train = synthetic_mnist(5, 256, 64, device=dev)
+    test = synthetic_mnist(6, 128, 64, device=dev)
+    init = torch.tensor(init_vector(3, 2797010, 0.03))
+
+    def fresh(logdir):
+        net = MLP()
+        with torch.no_grad():
+            torch.nn.utils.vector_to_parameters(init.clone(), net.parameters())
+        hp = dict(prior_sig=1.0, bias="informative", Ninflate=1.0, nd=0.05, burnin=0, thin=1,
+                  nst=1, momentum_decay=0.18)
+        args = SimpleNamespace(device=dev, ND=1000, pretrained=None, lr=1e-2, lr_head=2e-2,
+                               momentum=0.0, epochs=4, num_cycles=2, proportion_exploration=0.5,
+                               full_sample=False, test_eval_freq=1, ece_num_bins=15,
+                               log_dir=str(logdir), num_classes=10, noise_mode="philox", seed=77,
+                               resume_state=True,
+                               hparams={k: str(v) for k, v in hp.items()})
+        return csghmc.Runner(net.to(dev), None, args, logging.getLogger("resume"))
+
+    a = fresh(tmp_path / "a")
+    os.makedirs(tmp_path / "a", exist_ok=True)
+    a.train(train, None, test)
+    torch.cuda.synchronize()
+    ck = os.path.join(tmp_path / "a", "1_ckpt.pt")
+    assert os.path.exists(ck)
+
+    os.makedirs(tmp_path / "b", exist_ok=True)
+    b = fresh(tmp_path / "b")
+    epoch = b.load_ckpt(ck, resume=True)
+    assert epoch == 1
+    b.train(train, None, test, start_epoch=epoch + 1)
+    torch.cuda.synchronize()
+    assert torch.equal(b.model.flat.theta, a.model.flat.theta)
+    assert torch.equal(b.model.flat.mom, a.model.flat.mom)
+    assert b.samples_per_cycle == a.samples_per_cycle
+    assert b.samples_collected == a.samples_collected
+    for c in a.cycle_theta_mom1:
+        assert torch.equal(b.cycle_theta_mom1[c].to(dev), a.cycle_theta_mom1[c])
+        assert torch.equal(b.cycle_theta_mom2[c].to(dev), a.cycle_theta_mom2[c])
