@@ -252,14 +252,17 @@ def reinit_network(net):
         net.apply(init)
 
 
-def resume_state(model, st, **counters):
+def resume_state(model, st, sgd=None, **counters):
     """What an exact continuation of a chain needs beyond the reference's
-    checkpoint keys: the momentum / SGD buffer, the sampler's step counter
-    (the Philox noise key), host counters and the torch RNG states (the
+    checkpoint keys: the momentum / SGD buffer, further per-element sampler
+    state (Adam m / v, its SGD buffer), the sampler's step counter (the Philox
+    noise key) and Adam's t, host counters, and the torch RNG states (the
     "torch" noise mode draws from them)."""
     out = {"mom": None if st.mom is None else st.mom.detach().clone(),
+           "extra": {k: v.detach().clone() for k, v in getattr(st, "extra", {}).items()},
            "step_count": int(model.step_count), "seed": int(model.seed),
-           "chain": int(model.chain),
+           "chain": int(model.chain), "t": getattr(model, "t", None),
+           "sgd_has_buffer": None if sgd is None else bool(sgd.has_buffer),
            "rng_cpu": torch.get_rng_state()}
     if torch.cuda.is_available():
         out["rng_cuda"] = torch.cuda.get_rng_state(st.device)
@@ -267,21 +270,32 @@ def resume_state(model, st, **counters):
     return out
 
 
-def restore_resume_state(model, st, ckpt):
-    """Inverse of resume_state (plus theta from the checkpoint's last_theta),
+def restore_resume_state(model, st, ckpt, sgd=None):
+    """Inverse of resume_state (plus theta from the checkpoint's last_theta —
+    a flat vector for the cyclical methods, a state_dict for sgld / sghmc),
     in place so the parameter and gradient views stay bound."""
     rs = ckpt.get("resume")
     if rs is None:
         raise RuntimeError("checkpoint has no resume state (save it with args.resume_state=True)")
+    last = ckpt["last_theta"]
+    if isinstance(last, dict):
+        last = torch.cat([last[nm].reshape(-1).to(st.theta.device) for nm in st.names])
     with torch.no_grad():
-        st.theta.copy_(ckpt["last_theta"].reshape(-1).to(st.theta.device))
+        st.theta.copy_(last.reshape(-1).to(st.theta.device))
         if rs.get("mom") is not None and st.mom is not None:
             st.mom.copy_(rs["mom"].to(st.mom.device))
+        for k, v in rs.get("extra", {}).items():
+            st.extra[k].copy_(v.to(st.extra[k].device))
     model.step_count = int(rs["step_count"])
     model.seed = int(rs["seed"])
     model.chain = int(rs["chain"])
+    if rs.get("t") is not None:
+        model.t = int(rs["t"])
+    if sgd is not None and rs.get("sgd_has_buffer") is not None:
+        sgd.has_buffer = bool(rs["sgd_has_buffer"])
     torch.set_rng_state(rs["rng_cpu"].cpu())
     if "rng_cuda" in rs and torch.cuda.is_available():
         torch.cuda.set_rng_state(rs["rng_cuda"].cpu(), st.device)
-    return {k: v for k, v in rs.items()
-            if k not in ("mom", "step_count", "seed", "chain", "rng_cpu", "rng_cuda")}
+    skip = ("mom", "extra", "step_count", "seed", "chain", "t", "sgd_has_buffer", "rng_cpu",
+            "rng_cuda")
+    return {k: v for k, v in rs.items() if k not in skip}

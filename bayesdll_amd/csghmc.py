@@ -268,9 +268,13 @@ class Runner:
         self.current_cycle = ckpt.get("current_cycle", 0)
         self.samples_per_cycle = ckpt.get("samples_per_cycle", {})
         if resume:
+            self.cycle_states = ckpt.get("cycle_states", self.cycle_states)
             st = self.model.state_for(self.net)
             extra = R.restore_resume_state(self.model, st, ckpt)
             self.samples_collected = extra.get("samples_collected", self.samples_collected)
+            # the checkpoint is written at a cycle's completion, before the
+            # cycle-end hook (momentum / optimizer reset, cold restart): replay it
+            self._cycle_completed(self.current_cycle)
         return ckpt["epoch"]
 
     def full_batch_likelihoods(self, train_loader):

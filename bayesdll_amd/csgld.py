@@ -93,7 +93,7 @@ class Runner:
     def _cycle_completed(self, cycle_number):
         """Hook after a newly completed cycle was scored and checkpointed."""
 
-    def train(self, train_loader, val_loader, test_loader):
+    def train(self, train_loader, val_loader, test_loader, start_epoch=0):
         args, logger = self.args, self.logger
         logger.info("Start training with Cyclical SGLD (fused MI355X kernel)...")
         losses_train = np.zeros(args.epochs)
@@ -104,7 +104,7 @@ class Runner:
         errors_val = np.zeros(args.epochs) if val_loader is not None else None
         best_loss = np.inf
         tic0 = time.time()
-        for ep in range(args.epochs):
+        for ep in range(start_epoch, args.epochs):
             self.cyclical_scheduler.current_epoch = ep
             tic = time.time()
             losses_train[ep], errors_train[ep], cycle_updated = self.train_one_epoch(train_loader)
@@ -221,16 +221,25 @@ class Runner:
                     "cycle_likelihoods": self.cycle_likelihoods,
                     "cycle_states": self.cycle_states,
                     "epoch": epoch, "current_cycle": self.current_cycle,
-                    "samples_per_cycle": self.samples_per_cycle}, fname)
+                    "samples_per_cycle": self.samples_per_cycle,
+                    **({"resume": R.resume_state(self.model, self._state(), sgd=self.sgd,
+                                                 samples_collected=self.samples_collected)}
+                       if getattr(self.args, "resume_state", False) else {})}, fname)
         return fname
 
-    def load_ckpt(self, ckpt_path):
+    def load_ckpt(self, ckpt_path, resume=False):
+        """methods/csgld.py (same keys restored); resume=True as in csghmc."""
         ckpt = R.load_checkpoint(ckpt_path, self.args.device)
         self.cycle_theta_mom1 = ckpt.get("cycle_theta_mom1", {})
         self.cycle_theta_mom2 = ckpt.get("cycle_theta_mom2", {})
         self.cycle_likelihoods = ckpt.get("cycle_likelihoods", {})
         self.current_cycle = ckpt.get("current_cycle", 0)
         self.samples_per_cycle = ckpt.get("samples_per_cycle", {})
+        if resume:
+            self.cycle_states = ckpt.get("cycle_states", self.cycle_states)
+            extra = R.restore_resume_state(self.model, self._state(), ckpt, sgd=self.sgd)
+            self.samples_collected = extra.get("samples_collected", self.samples_collected)
+            self._cycle_completed(self.current_cycle)  # as csghmc.Runner.load_ckpt
         return ckpt["epoch"]
 
     def full_batch_likelihoods(self, train_loader):

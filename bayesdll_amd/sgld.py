@@ -117,7 +117,9 @@ class Runner:
                          div_mode=self.model.div_mode)
         self.post_theta_cnt = 1
 
-    def train(self, train_loader, val_loader, test_loader):
+    def train(self, train_loader, val_loader, test_loader, start_epoch=0):
+        """methods/sgld.py:69-190; start_epoch > 0 continues a chain restored
+        with load_ckpt(..., resume=True)."""
         args, logger = self.args, self.logger
         logger.info("Start training...")
         losses_train = np.zeros(args.epochs)
@@ -128,8 +130,8 @@ class Runner:
         errors_val = np.zeros(args.epochs) if val_loader is not None else None
         best_loss = np.inf
         tic0 = time.time()
-        bi = 0
-        for ep in range(args.epochs):
+        bi = start_epoch * len(train_loader)  # the global iteration count thinning uses
+        for ep in range(start_epoch, args.epochs):
             if ep == self.burnin:
                 logger.info("(leaving burnin period) start collecting posterior samples")
                 self.seed_moments()
@@ -231,21 +233,29 @@ class Runner:
                     "prior_sig": self.model.prior_sig,
                     "optimizer": self.optimizer.state_dict(),
                     **self._extra_ckpt(),
+                    **({"resume": R.resume_state(self.model, self._state(), sgd=self.sgd)}
+                       if getattr(self.args, "resume_state", False) else {}),
                     "epoch": epoch}, fname)
         return fname
 
-    def load_ckpt(self, ckpt_path, exact_count=False):
+    def load_ckpt(self, ckpt_path, exact_count=False, resume=False):
         """methods/sgld.py:388-398. The reference sets post_theta_cnt = epoch
         (:394); kept by default for drop-in parity, exact_count=True restores
-        the saved count instead."""
+        the saved count instead.  resume=True (checkpoint saved under
+        args.resume_state) restores theta, the sampler's buffers, step counter
+        and RNG states as well, so train(..., start_epoch=epoch + 1) continues
+        the chain exactly."""
         ckpt = R.load_checkpoint(ckpt_path, self.args.device)
         self.post_theta_mom1 = ckpt["post_theta_mom1"]
         if ckpt["post_theta_mom2"] is not None:
             self.post_theta_mom2 = ckpt["post_theta_mom2"]
-        self.post_theta_cnt = ckpt["post_theta_cnt"] if exact_count else ckpt["epoch"]
+        exact = exact_count or resume
+        self.post_theta_cnt = ckpt["post_theta_cnt"] if exact else ckpt["epoch"]
         self.model.prior_sig = ckpt["prior_sig"]
         self.optimizer.load_state_dict(ckpt["optimizer"])
         self._load_extra(ckpt)
+        if resume:
+            R.restore_resume_state(self.model, self._state(), ckpt, sgd=self.sgd)
         return ckpt["epoch"]
 
     # checkpoint hooks: SGLD's flat state.mom is the SGD momentum buffer

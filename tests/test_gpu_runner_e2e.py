@@ -386,3 +386,81 @@ def test_csghmc_exact_resume_from_checkpoint(tmp_path):
     for c in a.cycle_theta_mom1:
         assert torch.equal(b.cycle_theta_mom1[c].to(dev), a.cycle_theta_mom1[c])
         assert torch.equal(b.cycle_theta_mom2[c].to(dev), a.cycle_theta_mom2[c])
+
+
+@pytest.mark.parametrize("method", ["sgld", "sghmc", "adam_sghmc", "csgld", "adam_csghmc",
+                                    "csghmc_fs"])
+def test_exact_resume_all_runners(method, tmp_path):
+    """args.resume_state for every Runner: a chain restored from an epoch-1
+    checkpoint and continued with train(start_epoch=2) ends bit-for-bit where
+    the uninterrupted 4-epoch run does — theta, momentum, the extra buffers
+    (Adam m/v, SGD buffer), the step counter and the posterior moments.  The
+    SGLD family writes ckpt.pt only on a new best loss, so the test snapshots
+    it at the end of epoch 1; the cyclical family writes 1_ckpt.pt at the end
+    of cycle 1 (= epoch 1), before the cycle-end hook that resume replays
+    (optimizer reset, cold restart)."""
+    import importlib
+    import os
+    import shutil
+    mod = importlib.import_module(f"bayesdll_amd.{method}")
+    dev = "cuda"
+    train = synthetic_mnist(5, 256, 64, device=dev)
+    test = synthetic_mnist(6, 128, 64, device=dev)
+    init = torch.tensor(init_vector(4, 2797010, 0.03))
+    cyclical = method in ("csgld", "adam_csghmc", "csghmc_fs")
+
+    def fresh(logdir):
+        os.makedirs(logdir, exist_ok=True)
+        net = MLP()
+        with torch.no_grad():
+            torch.nn.utils.vector_to_parameters(init.clone(), net.parameters())
+        hp = dict(prior_sig=1.0, bias="informative", Ninflate=1.0, nd=0.05, burnin=1, thin=2,
+                  nst=2, momentum_decay=0.18, perform_cold_restarts="true")
+        args = SimpleNamespace(device=dev, ND=1000, pretrained=None, lr=1e-2, lr_head=2e-2,
+                               momentum=0.5, epochs=4, num_cycles=2, proportion_exploration=0.5,
+                               full_sample=False, test_eval_freq=1, ece_num_bins=15,
+                               log_dir=str(logdir), num_classes=10, noise_mode="philox",
+                               seed=91, resume_state=True,
+                               hparams={k: str(v) for k, v in hp.items()})
+        return mod.Runner(net.to(dev), None, args, logging.getLogger("resume"))
+
+    a = fresh(tmp_path / "a")
+    snap = str(tmp_path / "snap.pt")
+    if cyclical:
+        a.train(train, None, test)
+        shutil.copy(os.path.join(tmp_path / "a", "1_ckpt.pt"), snap)
+    else:
+        orig = a.train_one_epoch
+
+        def snapshot_after_epoch1(loader, collect, bi):
+            out = orig(loader, collect, bi)
+            if out[2] == 2 * len(loader):
+                a.save_ckpt(1)
+                shutil.copy(os.path.join(tmp_path / "a", "ckpt.pt"), snap)
+            return out
+        a.train_one_epoch = snapshot_after_epoch1
+        a.train(train, None, test)
+    torch.cuda.synchronize()
+
+    b = fresh(tmp_path / "b")
+    epoch = b.load_ckpt(snap, resume=True)
+    assert epoch == 1
+    b.train(train, None, test, start_epoch=epoch + 1)
+    torch.cuda.synchronize()
+    sa, sb = a.model.flat, b.model.flat
+    assert torch.equal(sb.theta, sa.theta)
+    assert torch.equal(sb.mom, sa.mom)
+    assert set(sb.extra) == set(sa.extra)
+    for k in sa.extra:
+        assert torch.equal(sb.extra[k], sa.extra[k]), k
+    assert b.model.step_count == a.model.step_count
+    assert getattr(b.model, "t", None) == getattr(a.model, "t", None)
+    if cyclical:
+        assert b.samples_per_cycle == a.samples_per_cycle
+        for c in a.cycle_theta_mom1:
+            assert torch.equal(b.cycle_theta_mom1[c].to(dev), a.cycle_theta_mom1[c])
+            assert torch.equal(b.cycle_theta_mom2[c].to(dev), a.cycle_theta_mom2[c])
+    else:
+        assert b.post_theta_cnt == a.post_theta_cnt
+        assert torch.equal(b.post_theta_mom1, a.post_theta_mom1)
+        assert torch.equal(b.post_theta_mom2, a.post_theta_mom2)
