@@ -50,6 +50,18 @@ def init_chains(backend=None):
     return rank(), world(), device
 
 
+def _all_reduce_sum(t):
+    """all_reduce(SUM) in place.  gloo (CPU tests, ranks sharing one GPU) is
+    fed a host copy of a device tensor; RCCL ("nccl") reduces on the device."""
+    if t.is_cuda and dist.get_backend() == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
 def chain_seed(base_seed):
     """Per-chain seed: base + rank (each chain its own Philox key)."""
     return int(base_seed) + rank()
@@ -60,8 +72,7 @@ def average_predictive(logp):
     k = world()
     if k == 1:
         return logp
-    p = logp.float().exp()
-    dist.all_reduce(p, op=dist.ReduceOp.SUM)
+    p = _all_reduce_sum(logp.float().exp())
     return (p / k).log()
 
 
@@ -71,9 +82,14 @@ def gather_logits(logits_all):
     k = world()
     if k == 1:
         return logits_all
-    parts = [torch.empty_like(logits_all) for _ in range(k)]
-    dist.all_gather(parts, logits_all.contiguous())
-    return torch.cat(parts, dim=2)
+    src = logits_all.contiguous()
+    host = src.is_cuda and dist.get_backend() == "gloo"
+    if host:
+        src = src.cpu()
+    parts = [torch.empty_like(src) for _ in range(k)]
+    dist.all_gather(parts, src)
+    out = torch.cat(parts, dim=2)
+    return out.to(logits_all.device) if host else out
 
 
 def pool_moments(mom1, mom2=None, count=1.0):
@@ -92,14 +108,13 @@ def pool_moments(mom1, mom2=None, count=1.0):
     if k == 1:
         return mom1.clone(), (None if mom2 is None else mom2.clone())
     tot = torch.tensor([c], dtype=torch.float64, device=mom1.device)
-    dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    _all_reduce_sum(tot)
     scale = c / float(tot.item())
     out = []
     for m in (mom1, mom2):
         if m is None:
             out.append(None)
             continue
-        w = m * scale
-        dist.all_reduce(w, op=dist.ReduceOp.SUM)
+        w = _all_reduce_sum(m * scale)
         out.append(w)
     return out[0], out[1]
