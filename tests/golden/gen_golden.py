@@ -450,12 +450,96 @@ def run_mlp(methods, method, cfg):
     return out
 
 
+# --------------------------------------------------------------------------
+# Checkpoint interop: a checkpoint WRITTEN BY THE
+# REFERENCE Runner, then loaded into a FRESH reference Runner and evaluated.
+# The product must load the same file (weights_only) and predict the same.
+# A narrow mlp (width 16) keeps the .pt fixtures small; noise is the
+# deterministic det_normal stream (draw counter restarted at 0 for the
+# evaluation), which the product replays with its "external" noise source.
+# --------------------------------------------------------------------------
+CKPT_CONFIGS = {
+    "csghmc": dict(epochs=4, ntrain=256, ntest=128, batch=64, num_cycles=2, beta=0.5, lr=0.02,
+                   lr_head=0.02, ND=256, data_seed=21, init_seed=22, noise_seed=23,
+                   eval_noise_seed=24, width=16, ckpt="2_ckpt.pt",
+                   hparams=dict(prior_sig=1.0, bias="informative", momentum_decay=0.18,
+                                Ninflate=1.0, nd=0.01, burnin=0, thin=1, nst=2)),
+    "sgld": dict(epochs=3, ntrain=256, ntest=128, batch=64, lr=1e-2, lr_head=1e-2, momentum=0.5,
+                 ND=256, data_seed=25, init_seed=26, noise_seed=27, eval_noise_seed=28, width=16,
+                 ckpt="ckpt.pt",
+                 hparams=dict(prior_sig=1.0, bias="informative", Ninflate=1e3, nd=1.0, burnin=1,
+                              thin=1, nst=2)),
+}
+
+
+def run_ckpt_interop(methods, method, cfg):
+    import shutil
+    from networks import small_nets
+    mod = getattr(methods, method)
+    train = synthetic_mnist(cfg["data_seed"], cfg["ntrain"], cfg["batch"])
+    test = synthetic_mnist(cfg["data_seed"] + 100, cfg["ntest"], cfg["batch"])
+    counter = [0]
+    seed = [cfg["noise_seed"]]
+    orig = torch.randn_like
+
+    def det_randn_like(t, *a, **k):
+        out = torch.from_numpy(det_normal(seed[0], counter[0], t.numel())).reshape(t.shape)
+        counter[0] += 1
+        return out.to(t.dtype)
+
+    def make_runner(init_seed):
+        torch.manual_seed(0)
+        net = small_nets.MLP(input_dim=784, output_dim=10, width=cfg["width"], depth=3)
+        net.readout_name = "classifier"
+        n = sum(p.numel() for p in net.parameters())
+        with torch.no_grad():
+            torch.nn.utils.vector_to_parameters(torch.tensor(init_vector(init_seed, n, 0.03)),
+                                                net.parameters())
+        tmp = tempfile.mkdtemp(prefix="bdl_golden_ckpt_")
+        args = make_args(tmp, epochs=cfg["epochs"], num_cycles=cfg.get("num_cycles", 2),
+                         lr=cfg["lr"], lr_head=cfg["lr_head"], momentum=cfg.get("momentum", 0.0),
+                         ND=cfg["ND"], proportion_exploration=cfg.get("beta", 0.5),
+                         test_eval_freq=1,
+                         hparams={k: str(v) for k, v in cfg["hparams"].items()})
+        return mod.Runner(net, None, args, logging.getLogger("golden")), tmp
+
+    torch.randn_like = det_randn_like
+    try:
+        runner, tmp = make_runner(cfg["init_seed"])
+        runner.train(train, None, test)
+        src = os.path.join(tmp, cfg["ckpt"])
+        dst = os.path.join(HERE, f"ckpt_ref_{method}.pt")
+        shutil.copyfile(src, dst)
+        # a fresh Runner (different init) restores the file and evaluates
+        fresh, _ = make_runner(cfg["init_seed"] + 1000)
+        epoch = fresh.load_ckpt(dst)
+        seed[0], counter[0] = cfg["eval_noise_seed"], 0
+        loss, err, targets, logits, logits_all = fresh.evaluate(test)
+        draws = counter[0]
+    finally:
+        torch.randn_like = orig
+    return dict(config=json.dumps(dict(cfg, method=method)), epoch=np.int64(epoch),
+                eval_loss=np.float64(loss), eval_err=np.float64(err), targets=targets,
+                logits=logits.astype(np.float32), logits_all=logits_all.astype(np.float32),
+                eval_draws=np.int64(draws))
+
+
 def main():
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
     logging.basicConfig(level=logging.WARNING)
     methods = import_reference()
     torch.set_num_threads(1)
     only = os.environ.get("GOLDEN_ONLY")
+    if only == "ckpt":
+        torch.set_num_threads(8)
+        recs = {}
+        for method, cfg in CKPT_CONFIGS.items():
+            rec = run_ckpt_interop(methods, method, copy.deepcopy(cfg))
+            recs.update({f"{method}_{k}": v for k, v in rec.items()})
+            print(f"wrote ckpt_ref_{method}.pt epoch={int(rec['epoch'])} "
+                  f"eval_draws={int(rec['eval_draws'])} loss={float(rec['eval_loss']):.6f}")
+        np.savez_compressed(os.path.join(HERE, "ckpt_ref.npz"), **recs)
+        return
     if only == "mlp":
         torch.set_num_threads(8)
         for name, (method, cfg) in MLP_CONFIGS.items():

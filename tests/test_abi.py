@@ -228,3 +228,24 @@ def test_missing_library_fails_loudly():
     out = subprocess.run(["python", "-c", code], env=env, capture_output=True, text=True,
                          cwd=os.path.dirname(HEADER) + "/..", timeout=300)
     assert "raised" in out.stdout and "libbdl_sgmcmc" in out.stdout, out.stdout + out.stderr
+
+
+def test_reference_written_checkpoints_load_weights_only():
+    """The reference-written checkpoint fixtures (tests/golden/ckpt_ref_*.pt)
+    load through the product's loader (torch.load weights_only=True plus the
+    numpy types csghmc's cycle_likelihoods hold): nothing is unpickled as code.
+    Keys are the reference's (methods/csghmc.py:530-549, methods/sgld.py:367-385)."""
+    import os
+    import torch
+    from bayesdll_amd._runner import load_checkpoint
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    ck = load_checkpoint(os.path.join(golden, "ckpt_ref_csghmc.pt"), "cpu")
+    assert set(ck) == {"last_theta", "cycle_theta_mom1", "cycle_theta_mom2", "cycle_likelihoods",
+                       "cycle_states", "epoch", "current_cycle", "samples_per_cycle"}
+    assert sorted(ck["cycle_theta_mom1"]) == [1, 2] and ck["current_cycle"] == 2
+    assert ck["last_theta"].shape == ck["cycle_theta_mom1"][1].shape
+    ck = load_checkpoint(os.path.join(golden, "ckpt_ref_sgld.pt"), "cpu")
+    assert set(ck) == {"last_theta", "post_theta_mom1", "post_theta_mom2", "post_theta_cnt",
+                       "prior_sig", "optimizer", "epoch"}
+    n = sum(v.numel() for v in ck["last_theta"].values())
+    assert ck["post_theta_mom1"].numel() == n and isinstance(ck["post_theta_mom1"], torch.Tensor)

@@ -20,6 +20,7 @@ and noise stream).  Two kinds of checks:
   real autograd, by test_mlp_real_autograd_matches_reference_update_same_gpu
   below (same hardware for both sides -> 1e-5 north-star tolerance).
 """
+import json
 import logging
 import tempfile
 from types import SimpleNamespace
@@ -464,3 +465,49 @@ def test_exact_resume_all_runners(method, tmp_path):
         assert b.post_theta_cnt == a.post_theta_cnt
         assert torch.equal(b.post_theta_mom1, a.post_theta_mom1)
         assert torch.equal(b.post_theta_mom2, a.post_theta_mom2)
+
+
+@pytest.mark.parametrize("method", ["csghmc", "sgld"])
+def test_reference_written_checkpoint_loads_and_predicts_alike(method):
+    """Checkpoint interop: a checkpoint written by the
+    REFERENCE Runner (tests/golden/ckpt_ref_<method>.pt, gen_golden.py
+    GOLDEN_ONLY=ckpt) is loaded (weights_only) by a fresh product Runner, whose
+    evaluate() — GMM mixture / sample average over fused posterior draws —
+    must give the predictive the reference computed from the same file with a
+    fresh Runner and the same noise stream.  One forward pass per draw on a
+    different device: CROSS_HW_RTOL does not apply, 1e-4 does."""
+    import os
+    import bayesdll_amd.csghmc as csghmc
+    import bayesdll_amd.sgld as sgld
+    from golden_util import GOLDEN
+    fx = dict(np.load(os.path.join(GOLDEN, "ckpt_ref.npz"), allow_pickle=False))
+    cfg = json.loads(str(fx[f"{method}_config"]))
+    dev = "cuda"
+    torch.manual_seed(0)
+    net = MLP(width=cfg["width"])
+    n = sum(p.numel() for p in net.parameters())
+    with torch.no_grad():
+        torch.nn.utils.vector_to_parameters(
+            torch.tensor(init_vector(cfg["init_seed"] + 1000, n, 0.03)), net.parameters())
+    net = net.to(dev)
+    test = synthetic_mnist(cfg["data_seed"] + 100, cfg["ntest"], cfg["batch"], device=dev)
+    args = SimpleNamespace(device=dev, ND=cfg["ND"], pretrained=None, lr=cfg["lr"],
+                           lr_head=cfg["lr_head"], momentum=cfg.get("momentum", 0.0),
+                           epochs=cfg["epochs"], num_cycles=cfg.get("num_cycles", 2),
+                           proportion_exploration=cfg.get("beta", 0.5), full_sample=False,
+                           test_eval_freq=1, ece_num_bins=15, log_dir=tempfile.mkdtemp(),
+                           num_classes=10, noise_mode="external",
+                           hparams={k: str(v) for k, v in cfg["hparams"].items()})
+    mod = {"csghmc": csghmc, "sgld": sgld}[method]
+    runner = mod.Runner(net, None, args, logging.getLogger("interop"))
+    prov = DetProvider(cfg["eval_noise_seed"], [p.numel() for p in runner.net.parameters()])
+    runner.model.noise_provider = prov
+    epoch = runner.load_ckpt(os.path.join(GOLDEN, f"ckpt_ref_{method}.pt"))
+    assert epoch == int(fx[f"{method}_epoch"])
+    loss, err, targets, logits, logits_all = runner.evaluate(test)
+    assert prov.k == int(fx[f"{method}_eval_draws"])   # same number / order of draws
+    np.testing.assert_array_equal(targets, fx[f"{method}_targets"])
+    assert rel(logits, fx[f"{method}_logits"]) < 1e-4
+    assert rel(logits_all, fx[f"{method}_logits_all"]) < 1e-4
+    assert abs(loss - float(fx[f"{method}_eval_loss"])) < 1e-4 * float(fx[f"{method}_eval_loss"])
+    assert err == float(fx[f"{method}_eval_err"])
