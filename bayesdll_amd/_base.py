@@ -29,6 +29,7 @@ from . import _lib as L
 from .flat import FlatState
 
 NOISE_MODES = ("philox", "torch", "external")
+MAX_GRAPHS = 4  # captured forward/backward graphs per sampler (one per input shape)
 
 
 def default_noise_mode():
@@ -36,6 +37,11 @@ def default_noise_mode():
     if m not in NOISE_MODES:
         raise ValueError(f"BDL_NOISE_MODE must be one of {NOISE_MODES}, got {m!r}")
     return m
+
+
+def default_graph():
+    """BDL_GRAPH=1: replay forward + backward from a captured HIP graph."""
+    return os.environ.get("BDL_GRAPH", "0") not in ("", "0", "false", "False")
 
 
 def default_chain():
@@ -60,6 +66,8 @@ class FusedModelBase(nn.Module):
         self.chain = default_chain()
         self.step_count = 0
         self.div_mode = None
+        self.graph = default_graph()
+        self._graphs = {}
         self._state = None
         self._state_net = None
 
@@ -86,12 +94,82 @@ class FusedModelBase(nn.Module):
 
     # ----------------------------------------------------------- fwd/bwd
     def forward_backward(self, st, net, x, y, criterion):
+        if self.graph and x.is_cuda and y.is_cuda and torch.is_grad_enabled():
+            got = self._graphed_forward_backward(st, net, x, y, criterion)
+            if got is not None:
+                return got
         out = net(x)
         loss = criterion(out, y)
         st.zero_grad()          # in place of net.zero_grad(): .grad stays a flat view
         loss.backward()
         st.sync_grads()
         return loss, out
+
+    def _graphed_forward_backward(self, st, net, x, y, criterion):
+        """Forward + loss + backward replayed from a captured HIP graph
+        (torch.cuda.CUDAGraph = hipGraph on ROCm): one graph launch instead of
+        one host launch per kernel, which is what bounds a small network's step
+        (mlp_mnist: tools/e2e_compare.py).  The graph zeroes the flat gradient
+        buffer and lets autograd accumulate into its views, exactly the eager
+        ops, so a step is bit-identical to eager mode for networks whose
+        forward has no random ops.  Assumes a static network: which parameters
+        get a gradient is fixed at capture (the eager path re-checks it every
+        step, like the reference's `if p.grad is not None`).  One graph per
+        (input shape, dtype, train mode, criterion), at most MAX_GRAPHS;
+        beyond that, or when the gradient views were re-bound, eager."""
+        key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, net.training, id(criterion),
+               id(net))
+        g = self._graphs.get(key)
+        if g is None:
+            if len(self._graphs) >= MAX_GRAPHS:
+                return None
+            g = self._capture(st, net, x, y, criterion)
+            self._graphs[key] = g
+        if any(p.grad is not gt for p, gt in zip(st.params, g["grads"])):
+            self._graphs.clear()    # user code re-bound .grad: recapture on the next step
+            return None
+        g["x"].copy_(x)
+        g["y"].copy_(y)
+        g["graph"].replay()
+        st._touched[:] = g["touched"]
+        st._select_runs(g["untouched"])
+        return g["loss"], g["out"].detach().clone()
+
+    def _capture(self, st, net, x, y, criterion):
+        sx, sy = x.detach().clone(), y.detach().clone()
+        # warm-up passes on a side stream (library handles, autotuned kernels)
+        # must not move the network's state: keep buffers (BatchNorm running
+        # statistics) and the device RNG as they were
+        bufs = [b.detach().clone() for b in net.buffers()]
+        rng = torch.cuda.get_rng_state(st.device)
+        side = torch.cuda.Stream(st.device)
+        side.wait_stream(torch.cuda.current_stream(st.device))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                st.zero_grad()
+                criterion(net(sx), sy).backward()
+        torch.cuda.current_stream(st.device).wait_stream(side)
+        with torch.no_grad():
+            for b, c in zip(net.buffers(), bufs):
+                b.copy_(c)
+        torch.cuda.set_rng_state(rng, st.device)
+        st.zero_grad()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            st.grad.zero_()
+            out = net(sx)
+            loss = criterion(out, sy)
+            loss.backward()
+        st.sync_grads()  # gradient views intact; which parameters got a gradient
+        untouched = tuple(i for i, ptr in enumerate(st._grad_ptrs)
+                          if ptr is not None and st._touched and not st._touched[i])
+        # keep the static outputs, not the captured autograd graph: its
+        # AccumulateGrad nodes would otherwise outlive the capture and meet the
+        # next capture's warm-up on another stream
+        out, loss = out.detach(), loss.detach()
+        return {"graph": graph, "x": sx, "y": sy, "out": out, "loss": loss,
+                "grads": [p.grad for p in st.params], "touched": list(st._touched),
+                "untouched": untouched}
 
     # -------------------------------------------------------------- noise
     def draw_noise(self, st):

@@ -55,6 +55,8 @@ class Runner:
             self.model.noise_mode = args.noise_mode
         if hasattr(args, "seed") and args.seed is not None:
             self.model.seed = int(args.seed)
+        if getattr(args, "graph", None) is not None:
+            self.model.graph = bool(args.graph)
 
         # lr holder with the reference's two param groups (body, head)
         self.optimizer = torch.optim.SGD(

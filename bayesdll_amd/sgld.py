@@ -83,6 +83,8 @@ class Runner:
             self.model.noise_mode = args.noise_mode
         if getattr(args, "seed", None) is not None:
             self.model.seed = int(args.seed)
+        if getattr(args, "graph", None) is not None:
+            self.model.graph = bool(args.graph)
         self.optimizer = torch.optim.SGD(
             [{"params": [p for pn, p in self.net.named_parameters()
                          if self.net.readout_name not in pn], "lr": args.lr},

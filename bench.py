@@ -169,7 +169,7 @@ def cpu_baseline(segs, readout, seconds):
                       f"randn_like noise) in {el:.1f} s on {cpu_model}"}
 
 
-def e2e_steps(steps, warmup, local, seed):
+def e2e_steps(steps, warmup, local, seed, graph=False):
     """Informational: full cSGHMC steps on a real ViT-L/32 (random init,
     synthetic [16,3,224,224] batch): forward + backward (PyTorch-ROCm fp32
     autograd, gradients written into the flat buffer) + the fused update.
@@ -181,6 +181,7 @@ def e2e_steps(steps, warmup, local, seed):
     net = backbone("vit_l_32", 1000).to(dev)
     model = csghmc.Model(ND=1840, prior_sig=1.0, momentum_decay=0.18)
     model.noise_mode = "philox"
+    model.graph = graph  # forward + backward replayed from a captured HIP graph
     crit = torch.nn.CrossEntropyLoss()
     g = torch.Generator(device=dev).manual_seed(seed)
     x = torch.randn(16, 3, 224, 224, device=dev, generator=g)
@@ -450,6 +451,9 @@ def main():
         torch.cuda.empty_cache()
         e2e = e2e_steps(a.e2e_steps, 3, local, 42)
         e2e["fused_update_share"] = round(dom["avg_ms"] / e2e["ms_per_step"], 4)
+        eg = e2e_steps(a.e2e_steps, 3, local, 42, graph=True)
+        e2e["graph_ms_per_step"] = eg["ms_per_step"]
+        e2e["graph_steps_per_s"] = eg["steps_per_s"]
         out["e2e"] = e2e
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not sgld:
         out["cpu_baseline"] = cpu_baseline(segs, readout, a.cpu_baseline_seconds)

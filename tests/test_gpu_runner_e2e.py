@@ -511,3 +511,90 @@ def test_reference_written_checkpoint_loads_and_predicts_alike(method):
     assert rel(logits_all, fx[f"{method}_logits_all"]) < 1e-4
     assert abs(loss - float(fx[f"{method}_eval_loss"])) < 1e-4 * float(fx[f"{method}_eval_loss"])
     assert err == float(fx[f"{method}_eval_err"])
+
+
+@pytest.mark.parametrize("method", ["csghmc", "sgld"])
+def test_graph_mode_is_bit_identical_to_eager(method):
+    """Model.graph (BDL_GRAPH=1): forward + backward replayed from a captured
+    HIP graph gives the eager chain bit for bit (same kernels, same order),
+    including a ragged last batch (a second graph) and the loss values the
+    Runner logs."""
+    import bayesdll_amd.csghmc as csghmc
+    import bayesdll_amd.sgld as sgld
+    from bayesdll_amd.sgld import FusedSGD
+    dev = "cuda"
+    n = 2797010
+    init = torch.tensor(init_vector(31, n, 0.03))
+    data = synthetic_mnist(32, 200, 64, device=dev)   # batches of 64, 64, 64, 8
+    lrs = [1e-2, 2e-2]
+    crit = torch.nn.CrossEntropyLoss()
+
+    def run(graph):
+        net = MLP()
+        with torch.no_grad():
+            torch.nn.utils.vector_to_parameters(init.clone(), net.parameters())
+        net = net.to(dev)
+        if method == "csghmc":
+            model = csghmc.Model(30000.0, prior_sig=1.0, momentum_decay=0.18)
+        else:
+            model = sgld.Model(30000.0, prior_sig=1.0)
+            opt = torch.optim.SGD(net.parameters(), lr=lrs[0], momentum=0.5)
+            fsgd = FusedSGD(opt, 0.5)
+        model.noise_mode, model.seed, model.graph = "philox", 5, graph
+        losses, outs = [], []
+        for ep in range(3):
+            for k, (x, y) in enumerate(data):
+                if method == "csghmc":
+                    lo, out = model(x, y, net, None, crit, lrs, 1.0, 0.5, should_sample=(k % 2 == 0))
+                else:
+                    lo, out = model(x, y, net, None, crit, lrs, 1.0, 0.5, sgd=fsgd)
+                losses.append(lo)
+                outs.append(out.cpu())
+        torch.cuda.synchronize()
+        return model, model.flat.theta.cpu().numpy(), losses, outs
+
+    m_e, th_e, lo_e, out_e = run(False)
+    m_g, th_g, lo_g, out_g = run(True)
+    assert len(m_g._graphs) == 2 and not m_e._graphs
+    assert lo_g == lo_e
+    for a, b in zip(out_g, out_e):
+        assert torch.equal(a, b)
+    np.testing.assert_array_equal(th_g, th_e)
+
+
+@pytest.mark.parametrize("method", ["sgld", "csghmc_fs", "adam_csghmc"])
+def test_runner_graph_mode_matches_eager(method, tmp_path):
+    """args.graph=True through a whole Runner.train(): SGD momentum (sgld),
+    momentum resets + cold restarts drawn from the device RNG (csghmc_fs,
+    adam_csghmc), evaluations between epochs — the chain and the logged
+    losses equal the eager run's bit for bit."""
+    import importlib
+    mod = importlib.import_module(f"bayesdll_amd.{method}")
+    dev = "cuda"
+    train = synthetic_mnist(13, 256, 64, device=dev)
+    test = synthetic_mnist(14, 128, 64, device=dev)
+    hp = dict(prior_sig=1.0, bias="informative", Ninflate=1.0, nd=0.01, burnin=1, thin=2,
+              nst=2, momentum_decay=0.18, perform_cold_restarts="true")
+
+    def run(graph, sub):
+        torch.manual_seed(0)
+        net = MLP().to(dev)
+        args = SimpleNamespace(device=dev, ND=1000, pretrained=None, lr=1e-2, lr_head=2e-2,
+                               momentum=0.5, epochs=4, num_cycles=2, proportion_exploration=0.5,
+                               full_sample=False, test_eval_freq=1, ece_num_bins=15,
+                               log_dir=str(tmp_path / sub), num_classes=10, seed=11, graph=graph,
+                               hparams={k: str(v) for k, v in hp.items()})
+        (tmp_path / sub).mkdir()
+        runner = mod.Runner(net, None, args, logging.getLogger("graph"))
+        res = runner.train(train, None, test)
+        torch.cuda.synchronize()
+        return runner, res
+
+    r_e, res_e = run(False, "eager")
+    r_g, res_g = run(True, "graph")
+    assert r_g.model._graphs and not r_e.model._graphs
+    np.testing.assert_array_equal(r_g.model.flat.theta.cpu().numpy(),
+                                  r_e.model.flat.theta.cpu().numpy())
+    if res_e is not None:
+        np.testing.assert_array_equal(res_g["losses_train"], res_e["losses_train"])
+        np.testing.assert_array_equal(res_g["losses_test"], res_e["losses_test"])

@@ -31,15 +31,18 @@ def main():
     batch = int(os.environ.get("BATCH", "16"))
     steps = int(os.environ.get("STEPS", "10"))
     dev = "cuda"
-    x = torch.randn(batch, 3, 224, 224, device=dev)
-    y = torch.randint(0, 1000, (batch,), device=dev)
+    classes = 10 if name == "mlp_mnist" else 1000
+    shape = (batch, 1, 28, 28) if name == "mlp_mnist" else (batch, 3, 224, 224)
+    x = torch.randn(*shape, device=dev)
+    y = torch.randint(0, classes, (batch,), device=dev)
     crit = torch.nn.CrossEntropyLoss()
     lrs = [1e-4, 1e-2]
     res = {}
-    for mode in ("reference_torch_ops", "fused"):
+    for mode in ("reference_torch_ops", "fused", "fused_graph"):
         torch.manual_seed(0)
-        net = backbone(name, 1000).to(dev)
+        net = backbone(name, classes).to(dev)
         model = csghmc.Model(ND=1840, prior_sig=1.0, momentum_decay=0.18)
+        model.graph = mode == "fused_graph"  # forward + backward from a captured HIP graph
         moms = {n: torch.zeros_like(p) for n, p in net.named_parameters()}
         fwdbwd = upd = 0.0
         for k in range(steps + 3):
@@ -47,7 +50,7 @@ def main():
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
             ss = k % 10 == 0
-            if mode == "fused":
+            if mode.startswith("fused"):
                 model(x, y, net, None, crit, lrs, 1.0, 0.01, should_sample=ss)
             else:
                 out = net(x)
@@ -60,14 +63,18 @@ def main():
         res[mode] = (time.perf_counter() - t0) / steps * 1e3
         # update-only timing
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        if mode == "fused":
+        if mode == "fused_graph":
+            pass
+        elif mode == "fused":
             from bayesdll_amd import _lib as L
             from bayesdll_amd import kernels as K
             st = model.flat
             e0.record()
+            h0 = time.perf_counter()
             for _ in range(steps):
                 K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=(1e-7, 1e-6),
                               noise_mode=L.NOISE_PHILOX, one_minus_alpha=0.82, prior_sig=1.0)
+            res["fused_host_us_per_call"] = (time.perf_counter() - h0) / steps * 1e6 * 1e-3
             e1.record()
         else:
             e0.record()
@@ -75,11 +82,13 @@ def main():
                 reference_update(net, moms, lrs, 1.0, 0.18, 1840.0, 0.01, True)
             e1.record()
         torch.cuda.synchronize()
-        res[mode + "_update_only"] = e0.elapsed_time(e1) / steps
+        if mode != "fused_graph":
+            res[mode + "_update_only"] = e0.elapsed_time(e1) / steps
         del net, model, moms
         torch.cuda.empty_cache()
     for k, v in res.items():
-        print(f"{name} batch {batch}: {k}: {v:.3f} ms/step")
+        print(f"{name} batch {batch}: {k}: {v:.3f} ms/step" if "host" not in k else
+              f"{name} batch {batch}: {k}: {v * 1e3:.1f} us (launch-side host time, no sync)")
 
 
 if __name__ == "__main__":
