@@ -222,50 +222,97 @@ struct MArgs {
   float ca, cb, inv_ca, inv_cb;
 };
 
+// Per-element moment update (the reference's op order; see collect_core for
+// the fused-step twin).  COLLECT / RECIP / M2 are compile-time.
+template <int COLLECT, bool RECIP>
+__device__ __forceinline__ void moments_elem(const MArgs& a, float x, float& p, float& q) {
+  if constexpr (COLLECT == BDL_COLLECT_WELFORD_INIT) {
+    p = x;
+    q = 0.f;
+  } else if constexpr (COLLECT == BDL_COLLECT_WELFORD) {
+    const float d = x - p;
+    p = p + (RECIP ? d * a.inv_ca : d / a.ca);
+    const float d2 = x - p;
+    q = q + d * d2;
+  } else if constexpr (COLLECT == BDL_COLLECT_MEAN_INIT) {
+    p = x;
+    q = x * x;
+  } else {  // MEAN
+    const float u = x + a.ca * p;
+    p = RECIP ? u * a.inv_cb : u / a.cb;
+    const float w = x * x + a.ca * q;
+    q = RECIP ? w * a.inv_cb : w / a.cb;
+  }
+}
+
+// Grid-stride sweep, U float4 groups per lane in flight: a block iteration
+// wholly inside the vector issues all its loads before any arithmetic, with no
+// bounds checks; only the last partial iteration takes the guarded path.
+template <int COLLECT, bool RECIP, bool M2, int U>
 __global__ __launch_bounds__(kBlock) void bdl_moments_kernel(const MArgs a) {
-  const int64_t ngroups = (a.n + 3) >> 2;
-  const float inv_ca = a.inv_ca, inv_cb = a.inv_cb;
-  for (int64_t gi = (int64_t)blockIdx.x * kBlock + threadIdx.x; gi < ngroups;
-       gi += (int64_t)gridDim.x * kBlock) {
-    const int64_t e = gi * 4;
-    const f4v t = ld4(a.theta, e, a.n);
-    f4v m1 = {0.f, 0.f, 0.f, 0.f}, m2 = m1;
-    if (a.collect == BDL_COLLECT_WELFORD || a.collect == BDL_COLLECT_MEAN) {
-      m1 = ld4(a.mom1, e, a.n);
-      if (a.mom2) m2 = ld4(a.mom2, e, a.n);
-    }
+  constexpr bool kRead = COLLECT == BDL_COLLECT_WELFORD || COLLECT == BDL_COLLECT_MEAN;
+  constexpr int64_t kIter = (int64_t)kBlock * U;
+  const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {
+    const bool fast = gb + kIter <= nfull;
+    f4v t[U], m1[U], m2[U];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float x = t[j];
-      float p = m1[j], q = m2[j];
-      switch (a.collect) {
-        case BDL_COLLECT_WELFORD_INIT:
-          p = x;
-          q = 0.f;
-          break;
-        case BDL_COLLECT_WELFORD: {
-          const float d = x - p;
-          p = p + (a.recip ? d * inv_ca : d / a.ca);
-          const float d2 = x - p;
-          q = q + d * d2;
-          break;
+    for (int u = 0; u < U; ++u) {
+      const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+      const int64_t e = gi * 4;
+      m1[u] = m2[u] = t[u] = z;
+      if (fast) {
+        t[u] = vload(a.theta + e);
+        if constexpr (kRead) {
+          m1[u] = vload(a.mom1 + e);
+          if constexpr (M2) m2[u] = vload(a.mom2 + e);
         }
-        case BDL_COLLECT_MEAN_INIT:
-          p = x;
-          q = x * x;
-          break;
-        default: {  // MEAN
-          const float u = x + a.ca * p;
-          p = a.recip ? u * inv_cb : u / a.cb;
-          const float w = x * x + a.ca * q;
-          q = a.recip ? w * inv_cb : w / a.cb;
+      } else if (gi < ngroups) {
+        t[u] = ld4(a.theta, e, a.n);
+        if constexpr (kRead) {
+          m1[u] = ld4(a.mom1, e, a.n);
+          if constexpr (M2) m2[u] = ld4(a.mom2, e, a.n);
         }
       }
-      m1[j] = p;
-      m2[j] = q;
     }
-    st4(a.mom1, e, a.n, m1);
-    if (a.mom2) st4(a.mom2, e, a.n, m2);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+      const int64_t e = gi * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float p = m1[u][j], q = m2[u][j];
+        moments_elem<COLLECT, RECIP>(a, t[u][j], p, q);
+        m1[u][j] = p;
+        m2[u][j] = q;
+      }
+      if (fast) {
+        vstore(a.mom1 + e, m1[u]);
+        if constexpr (M2) vstore(a.mom2 + e, m2[u]);
+      } else if (gi < ngroups) {
+        st4(a.mom1, e, a.n, m1[u]);
+        if constexpr (M2) st4(a.mom2, e, a.n, m2[u]);
+      }
+    }
+  }
+}
+
+typedef void (*MomentsKernel)(const MArgs);
+
+template <int COLLECT>
+MomentsKernel pick_moments_c(bool recip, bool m2) {
+  constexpr int U = 4;
+  if (recip) return m2 ? bdl_moments_kernel<COLLECT, true, true, U> : bdl_moments_kernel<COLLECT, true, false, U>;
+  return m2 ? bdl_moments_kernel<COLLECT, false, true, U> : bdl_moments_kernel<COLLECT, false, false, U>;
+}
+
+MomentsKernel pick_moments(int collect, bool recip, bool m2) {
+  switch (collect) {
+    case BDL_COLLECT_WELFORD_INIT: return pick_moments_c<BDL_COLLECT_WELFORD_INIT>(recip, m2);
+    case BDL_COLLECT_WELFORD: return pick_moments_c<BDL_COLLECT_WELFORD>(recip, m2);
+    case BDL_COLLECT_MEAN_INIT: return pick_moments_c<BDL_COLLECT_MEAN_INIT>(recip, m2);
+    default: return pick_moments_c<BDL_COLLECT_MEAN>(recip, m2);
   }
 }
 
@@ -280,36 +327,96 @@ struct SArgs {
   uint64_t seed, chain, step;
 };
 
+// theta_s = m1 + sqrt(clamp(var, floor)) * eps.  VAR: where the variance
+// comes from (M2 = false: no second moment, var = floor — a single-sample
+// cycle, csghmc.py:456-458); RECIP: Welford M2 * fl(1/(n-1)) as torch on the
+// device; NOISE: buffer or in-register Philox.  Same sweep shape as the
+// moments kernel.
+template <int VAR, bool M2, bool RECIP>
+__device__ __forceinline__ float sample_var(const SArgs& a, float mj, float qj) {
+  float var;
+  if constexpr (!M2)
+    var = a.var_floor;
+  else if constexpr (VAR == BDL_VAR_RAW_MOMENTS)
+    var = a.ratio * (qj - mj * mj);  // sgld.py:342
+  else if constexpr (VAR == BDL_VAR_WELFORD)
+    var = RECIP ? qj * a.inv_ratio : qj / a.ratio;  // csghmc.py:455
+  else
+    var = qj;
+  if (!(var != var)) var = fmaxf(var, a.var_floor);  // clamp_(min=1e-12); NaN stays NaN
+  return var;
+}
+
+template <int VAR, bool M2, bool RECIP, int NOISE, int U>
 __global__ __launch_bounds__(kBlock) void bdl_sample_kernel(const SArgs a) {
-  const int64_t ngroups = (a.n + 3) >> 2;
-  for (int64_t gi = (int64_t)blockIdx.x * kBlock + threadIdx.x; gi < ngroups;
-       gi += (int64_t)gridDim.x * kBlock) {
-    const int64_t e = gi * 4;
-    const f4v m = ld4(a.mom1, e, a.n);
-    f4v q = {0.f, 0.f, 0.f, 0.f};
-    if (a.mom2) q = ld4(a.mom2, e, a.n);
-    const f4v eps = (a.noise_mode == BDL_NOISE_BUFFER)
-                        ? ld4(a.noise, e, a.n)
-                        : philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
-    f4v o;
+  constexpr int64_t kIter = (int64_t)kBlock * U;
+  const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {
+    const bool fast = gb + kIter <= nfull;
+    f4v m[U], q[U], ep[U];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float mj = m[j];
-      const float qj = q[j];
-      float var;
-      if (!a.mom2)
-        var = a.var_floor;  // single-sample cycle: ones*1e-12 (csghmc.py:456-458)
-      else if (a.var_mode == BDL_VAR_RAW_MOMENTS)
-        var = a.ratio * (qj - mj * mj);  // sgld.py:342
-      else if (a.var_mode == BDL_VAR_WELFORD)
-        var = a.inv_ratio != 0.0f ? qj * a.inv_ratio : qj / a.ratio;  // csghmc.py:455
-      else
-        var = qj;
-      if (!(var != var)) var = fmaxf(var, a.var_floor);  // clamp_(min=1e-12); NaN stays NaN
-      o[j] = mj + sqrtf(var) * eps[j];  // p_m + p_v.sqrt()*eps
+    for (int u = 0; u < U; ++u) {
+      const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+      const int64_t e = gi * 4;
+      m[u] = q[u] = ep[u] = z;
+      if (fast) {
+        m[u] = vload(a.mom1 + e);
+        if constexpr (M2) q[u] = vload(a.mom2 + e);
+        if constexpr (NOISE == BDL_NOISE_BUFFER) ep[u] = vload(a.noise + e);
+      } else if (gi < ngroups) {
+        m[u] = ld4(a.mom1, e, a.n);
+        if constexpr (M2) q[u] = ld4(a.mom2, e, a.n);
+        if constexpr (NOISE == BDL_NOISE_BUFFER) ep[u] = ld4(a.noise, e, a.n);
+      }
     }
-    st4(a.out, e, a.n, o);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+      const int64_t e = gi * 4;
+      if constexpr (NOISE == BDL_NOISE_PHILOX)
+        ep[u] = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+      f4v o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        o[j] = m[u][j] + sqrtf(sample_var<VAR, M2, RECIP>(a, m[u][j], q[u][j])) * ep[u][j];
+      if (fast)
+        vstore(a.out + e, o);
+      else if (gi < ngroups)
+        st4(a.out, e, a.n, o);
+    }
   }
+}
+
+typedef void (*SampleKernel)(const SArgs);
+
+// Posterior-sample geometry: Philox makes this sweep VALU-heavy per byte (12 B
+// per element against ~65 VALU slots), so it runs at its own occupancy —
+// 3 workgroups per CU, 4 float4 groups per lane in flight (tools/aux_sweep.py,
+// profiles/round1/aux_sweep.log) — independent of the step kernels' tuning.
+#ifndef BDL_SAMPLE_U
+#define BDL_SAMPLE_U 4
+#endif
+#ifndef BDL_SAMPLE_BPC
+#define BDL_SAMPLE_BPC 3
+#endif
+
+template <int NOISE>
+SampleKernel pick_sample_n(int var_mode, bool m2, bool recip) {
+  constexpr int U = BDL_SAMPLE_U;
+  if (!m2) return bdl_sample_kernel<BDL_VAR_GIVEN, false, false, NOISE, U>;
+  switch (var_mode) {
+    case BDL_VAR_RAW_MOMENTS: return bdl_sample_kernel<BDL_VAR_RAW_MOMENTS, true, false, NOISE, U>;
+    case BDL_VAR_WELFORD:
+      return recip ? bdl_sample_kernel<BDL_VAR_WELFORD, true, true, NOISE, U>
+                   : bdl_sample_kernel<BDL_VAR_WELFORD, true, false, NOISE, U>;
+    default: return bdl_sample_kernel<BDL_VAR_GIVEN, true, false, NOISE, U>;
+  }
+}
+
+SampleKernel pick_sample(int var_mode, bool m2, bool recip, int noise_mode) {
+  return noise_mode == BDL_NOISE_BUFFER ? pick_sample_n<BDL_NOISE_BUFFER>(var_mode, m2, recip)
+                                        : pick_sample_n<BDL_NOISE_PHILOX>(var_mode, m2, recip);
 }
 
 __global__ __launch_bounds__(kBlock) void bdl_philox_kernel(float* __restrict__ out, int64_t n,
@@ -339,6 +446,13 @@ StepKernel pick_step(int method, int noise, int collect, int unroll) {
 int grid_for(int64_t ngroups, int per_block_groups) {
   const int64_t want = (ngroups + per_block_groups - 1) / per_block_groups;
   const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
+  return (int)std::max<int64_t>(1, std::min(want, cap));
+}
+
+int grid_sample(int64_t ngroups) {
+  const int64_t per_block = (int64_t)kBlock * BDL_SAMPLE_U;
+  const int64_t want = (ngroups + per_block - 1) / per_block;
+  const int64_t cap = (int64_t)device_cu_count() * BDL_SAMPLE_BPC;
   return (int)std::max<int64_t>(1, std::min(want, cap));
 }
 
@@ -665,7 +779,8 @@ int bdl_moments_update(const bdl_moments_args* m, void* stream) {
   MArgs a{m->theta, m->mom1, m->mom2, m->n, m->collect, (m->flags & BDL_FLAG_RECIP_DIV) ? 1 : 0,
           m->collect_a, m->collect_b, recip_or(m->inv_collect_a, m->collect_a),
           recip_or(m->inv_collect_b, m->collect_b)};
-  hipLaunchKernelGGL(bdl_moments_kernel, dim3(grid_for((m->n + 3) / 4, kBlock * 4)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(pick_moments(m->collect, a.recip != 0, m->mom2 != nullptr),
+                     dim3(grid_for((m->n + 3) / 4, kBlock * 4)), dim3(kBlock), 0,
                      (hipStream_t)stream, a);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
@@ -688,7 +803,9 @@ int bdl_posterior_sample(const bdl_sample_args* s, void* stream) {
     if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_posterior_sample: vector not 16-B aligned");
   SArgs a{s->out, s->mom1, s->mom2, s->noise, s->n, s->var_mode, s->noise_mode,
           s->ratio, s->var_floor, s->inv_ratio, s->seed, s->chain, s->step};
-  hipLaunchKernelGGL(bdl_sample_kernel, dim3(grid_for((s->n + 3) / 4, kBlock * 4)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(pick_sample(s->var_mode, s->mom2 != nullptr, s->inv_ratio != 0.0f,
+                                 s->noise_mode),
+                     dim3(grid_sample((s->n + 3) / 4)), dim3(kBlock), 0,
                      (hipStream_t)stream, a);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) {

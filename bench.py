@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--grid-stride", type=int, default=-1)
     ap.add_argument("--no-autotune", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=10)
+    ap.add_argument("--no-aux", action="store_true",
+                    help="skip the posterior-sample / moments sweeps after the timed region")
     ap.add_argument("--prewarm-seconds", type=float, default=0.0,
                     help="untimed back-to-back launches before the measurement (clock ramp)")
     ap.add_argument("--no-placement", dest="placement", action="store_false",
@@ -133,6 +135,43 @@ def dist_setup():
         return dist, rank, world, local
     torch.cuda.set_device(local)
     return None, 0, 1, local
+
+
+def aux_kernels(st, reps=20):
+    """Informational, after the timed region: the other full-vector sweeps of
+    the path at the same size, HIP-event timed on the launch stream —
+    bdl_posterior_sample (theta_s = m1 + sqrt(var) * eps,
+    Welford variance, Philox noise; m1 r, m2 r, out w = 12 B/elem) and
+    bdl_moments_update (sgld.py:242-245 running mean / second moment: theta r,
+    m1 rw, m2 rw = 20 B/elem)."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    n = st.n
+    m1, m2, out = (torch.empty(n, dtype=torch.float32, device=st.device) for _ in range(3))
+    m1.copy_(st.theta)
+    m2.fill_(1e-6)
+    res = {}
+
+    def timed(name, nbytes, fn):
+        for _ in range(3):
+            fn(0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(reps):
+            fn(i + 3)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        gbs = nbytes * n / (ms * 1e-3) / 1e9
+        res[name] = {"avg_ms": round(ms, 4), "bytes_per_elem": nbytes, "gbs": round(gbs, 1),
+                     "frac": round(gbs / PEAK_HBM_GBS, 4)}
+
+    timed("posterior_sample", 12, lambda i: K.posterior_sample(
+        out, m1, m2, var_mode=L.VAR_WELFORD, ratio=4.0, seed=7, chain=0, step=i))
+    timed("moments_update", 20, lambda i: K.moments_update(
+        st.theta, m1, m2, L.COLLECT_MEAN, collect_a=float(i + 1), collect_b=float(i + 2)))
+    del m1, m2, out
+    return res
 
 
 def cpu_baseline(segs, readout, seconds):
@@ -446,6 +485,8 @@ def main():
                      "traffic": traffic,
                      "alg_bytes_per_launch": alg_bytes},
     }
+    if not a.no_aux:
+        out["aux_kernels"] = aux_kernels(st)
     if world == 1 and a.e2e_steps > 0 and a.backbone == "vit_l_32" and not sgld:
         del st, m1s, m2s
         torch.cuda.empty_cache()

@@ -638,3 +638,64 @@ def test_full_size_vit_csghmc_sample_and_welford_collect_bitexact():
         torch.cuda.synchronize()
         assert torch.equal(st.theta, th_ref) and torch.equal(st.mom, v_ref)
         assert torch.equal(m1, r1) and torch.equal(m2, r2)
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 7, 17, 1023, 2048, 2049, 4097, 65537, 1_000_003])
+def test_moments_and_sample_kernels_edge_sizes(n):
+    """Stand-alone moments (all four collect kinds, with and without m2) and
+    posterior-sample kernels (every variance source, Philox and buffer noise)
+    at sizes around the unrolled fast path's block iteration (256 lanes x U
+    float4 groups) and the float4 tail, vs the torch-on-device formulas."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    g = torch.Generator(device=DEV).manual_seed(n)
+    x = torch.randn(n, device=DEV, generator=g)
+    a1 = torch.randn(n, device=DEV, generator=g)
+    a2 = torch.rand(n, device=DEV, generator=g)
+    # Welford update, recip rounding (torch on the device: x * fl(1/5))
+    m1, m2 = a1.clone(), a2.clone()
+    K.moments_update(x, m1, m2, L.COLLECT_WELFORD, 5.0, div_mode="recip")
+    d = x - a1
+    e1 = a1 + d * (1.0 / 5.0)
+    e2 = a2 + d * (x - e1)
+    torch.cuda.synchronize()
+    assert torch.equal(m1, e1) and torch.equal(m2, e2)
+    # Welford init, with and without m2
+    m1, m2 = torch.full_like(x, 7.0), torch.full_like(x, 7.0)
+    K.moments_update(x, m1, m2, L.COLLECT_WELFORD_INIT)
+    torch.cuda.synchronize()
+    assert torch.equal(m1, x) and torch.equal(m2, torch.zeros_like(x))
+    m1 = torch.full_like(x, 7.0)
+    K.moments_update(x, m1, None, L.COLLECT_WELFORD_INIT)
+    torch.cuda.synchronize()
+    assert torch.equal(m1, x)
+    # running mean, true division, with and without m2
+    m1, m2 = a1.clone(), a2.clone()
+    K.moments_update(x, m1, m2, L.COLLECT_MEAN, 3.0, 4.0, div_mode="true")
+    torch.cuda.synchronize()
+    r1 = ((x + 3 * a1).cpu().double() / 4).float()
+    r2 = ((x * x + 3 * a2).cpu().double() / 4).float()
+    assert torch.equal(m1.cpu(), r1) and torch.equal(m2.cpu(), r2)
+    m1 = a1.clone()
+    K.moments_update(x, m1, None, L.COLLECT_MEAN, 3.0, 4.0, div_mode="recip")
+    torch.cuda.synchronize()
+    assert torch.equal(m1, (x + 3 * a1) * (1.0 / 4.0))
+    # posterior draws
+    eps = torch.randn(n, device=DEV, generator=g)
+    q = a1 ** 2 + a2
+    out = torch.full_like(x, float("nan"))
+    K.posterior_sample(out, a1, q, var_mode=L.VAR_WELFORD, ratio=3.0, noise=eps, div_mode="recip")
+    torch.cuda.synchronize()
+    assert torch.equal(out, a1 + (q * (1.0 / 3.0)).clamp(min=1e-12).sqrt() * eps)
+    K.posterior_sample(out, a1, a2, var_mode=L.VAR_GIVEN, noise=eps)
+    torch.cuda.synchronize()
+    assert torch.equal(out, a1 + a2.clamp(min=1e-12).sqrt() * eps)
+    # Philox noise = the stream bdl_philox_normal produces for the same key
+    K.posterior_sample(out, a1, q, var_mode=L.VAR_RAW_MOMENTS, ratio=1.25, seed=3, chain=1,
+                       step=9)
+    z = K.philox_normal(n, 3, 1, 9, device=DEV)
+    torch.cuda.synchronize()
+    assert torch.equal(out, a1 + (1.25 * (q - a1 * a1)).clamp(min=1e-12).sqrt() * z)
+    K.posterior_sample(out, a1, None, var_mode=L.VAR_WELFORD, seed=3, chain=1, step=9)
+    torch.cuda.synchronize()
+    assert torch.equal(out, a1 + torch.full_like(a1, 1e-12).sqrt() * z)
