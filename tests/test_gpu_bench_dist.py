@@ -1,0 +1,52 @@
+"""bench.py's N-rank path end to end on the box's one GPU: two ranks under
+torch.distributed.run with the gloo backend (BDL_BENCH_BACKEND=gloo, ranks
+sharing the device; RCCL needs one GPU per rank).  Checks the contract the
+driver relies on at N>1: one JSON line from rank 0, n_gpus = world size,
+value = all ranks' steps / max-over-ranks time, the evaluation collective
+(chains.average_predictive) timed after the timed region."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_bench_two_ranks_gloo():
+    env = dict(os.environ, BDL_BENCH_BACKEND="gloo", BDL_PLACEMENT_CANDIDATES="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5",
+           "--backbone", "resnet101", "--no-autotune", "--e2e-steps", "0"]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, (p.stdout + p.stderr)[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 20 and d["warmup"] == 5
+    assert d["scaling"] == "weak" and d["higher_is_better"] is True
+    assert d["value"] > 0 and abs(d["value"] - 2 * 20 / (d["ms_per_step"] * 20 / 1e3)) < 0.02 * d["value"]
+    assert d["config"]["parallelism"].startswith("2 independent chains")
+    ec = d["eval_collective"]
+    assert ec["backend"] == "gloo" and ec["finite"] is True
+    assert "cpu_baseline" not in d  # rank 0 at N=1 only
+    assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
