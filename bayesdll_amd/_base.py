@@ -100,18 +100,20 @@ class FusedModelBase(nn.Module):
                 return got
         out = net(x)
         loss = criterion(out, y)
-        st.zero_grad()          # in place of net.zero_grad(): .grad stays a flat view
+        st.zero_grad()          # in place of net.zero_grad() (FlatState.zero_grad)
         loss.backward()
-        st.sync_grads()
+        st.sync_grads()         # which tensors got a gradient, and where they live
         return loss, out
 
     def _graphed_forward_backward(self, st, net, x, y, criterion):
         """Forward + loss + backward replayed from a captured HIP graph
         (torch.cuda.CUDAGraph = hipGraph on ROCm): one graph launch instead of
         one host launch per kernel, which is what bounds a small network's step
-        (mlp_mnist: tools/e2e_compare.py).  The graph zeroes the flat gradient
-        buffer and lets autograd accumulate into its views, exactly the eager
-        ops, so a step is bit-identical to eager mode for networks whose
+        (mlp_mnist: tools/e2e_compare.py).  The graph holds exactly the eager
+        ops (in "tensor" gradient mode autograd's gradient tensors become
+        static graph outputs the kernel reads through the captured base table;
+        in "flat" mode the graph zeroes the flat buffer autograd accumulates
+        into), so a step is bit-identical to eager mode for networks whose
         forward has no random ops.  Assumes a static network: which parameters
         get a gradient is fixed at capture (the eager path re-checks it every
         step, like the reference's `if p.grad is not None`).  One graph per
@@ -131,8 +133,9 @@ class FusedModelBase(nn.Module):
         g["x"].copy_(x)
         g["y"].copy_(y)
         g["graph"].replay()
-        st._touched[:] = g["touched"]
-        st._select_runs(g["untouched"])
+        st.use_grad_table(g["table"])
+        if st._touched:
+            st._touched[:] = g["touched"]
         return g["loss"], g["out"].detach().clone()
 
     def _capture(self, st, net, x, y, criterion):
@@ -153,23 +156,22 @@ class FusedModelBase(nn.Module):
             for b, c in zip(net.buffers(), bufs):
                 b.copy_(c)
         torch.cuda.set_rng_state(rng, st.device)
-        st.zero_grad()
+        st.zero_grad()  # "tensor" mode: .grad = None, so the graph's gradients are its own
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            st.grad.zero_()
+            if st.grad is not None:  # "flat" mode: the graph zeroes the flat buffer
+                st.grad.zero_()
             out = net(sx)
             loss = criterion(out, sy)
             loss.backward()
-        st.sync_grads()  # gradient views intact; which parameters got a gradient
-        untouched = tuple(i for i, ptr in enumerate(st._grad_ptrs)
-                          if ptr is not None and st._touched and not st._touched[i])
+        st.sync_grads()  # the (static) gradient tensors' table; which parameters got one
         # keep the static outputs, not the captured autograd graph: its
         # AccumulateGrad nodes would otherwise outlive the capture and meet the
         # next capture's warm-up on another stream
         out, loss = out.detach(), loss.detach()
         return {"graph": graph, "x": sx, "y": sy, "out": out, "loss": loss,
                 "grads": [p.grad for p in st.params], "touched": list(st._touched),
-                "untouched": untouched}
+                "table": st.grad_table()}
 
     # -------------------------------------------------------------- noise
     def draw_noise(self, st):

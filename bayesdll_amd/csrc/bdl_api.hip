@@ -44,6 +44,8 @@ int fail(int code, const char* msg) {
   return code;
 }
 
+int fail(int code, const std::string& msg) { return fail(code, msg.c_str()); }
+
 // Tunables (bdl_set_launch_config).  blocks_per_cu * #CUs workgroups, each
 // lane keeps `unroll` float4 groups in flight per iteration.  Defaults (2
 // workgroups/CU, depth 1, grid-stride) from the gfx950 sweep (tools/sweep.py,
@@ -89,7 +91,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 template <int NOISE, bool RECIP, bool PRIOR>
 __device__ __forceinline__ double sqnorm_fast(const KArgs& a, const StepConst& c, int64_t gb,
-                                              float ns, double acc) {
+                                              float ns, double acc, const float* gp) {
   constexpr int U = 2;
   f4v th[U], g[U], t0[U], ep[U];
   const f4v z = {0.f, 0.f, 0.f, 0.f};
@@ -98,7 +100,7 @@ __device__ __forceinline__ double sqnorm_fast(const KArgs& a, const StepConst& c
     const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
     t0[u] = ep[u] = z;
     th[u] = vload(a.theta + e);
-    g[u] = vload(a.grad + e);
+    g[u] = vload(gp + e);
     if constexpr (PRIOR) t0[u] = vload(a.prior_mean + e);
     if constexpr (NOISE == BDL_NOISE_BUFFER) ep[u] = vload(a.noise + e);
   }
@@ -127,36 +129,37 @@ __device__ __forceinline__ void sqnorm_body(const KArgs& a, double* __restrict__
   c.inv_nd = a.inv_nd;
   c.inv_ca = c.inv_cb = c.clip_coef = 1.0f;
   const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
-  for (int i = threadIdx.x; i < a.nruns; i += kBlock) s_runs[i] = a.runs[i];
-  __syncthreads();
+  stage_runs(a);
   double acc = 0.0;
   int r = find_run_lds(a.nruns, (int64_t)blockIdx.x * kIter * 4);
   for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {
     while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
     const int64_t gend = min(gb + kIter, ngroups);
     const uint32_t attr = run_attr(r);
-    if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 && !(attr & BDL_ATTR_SKIP)) {
+    if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 && !(attr & kNoFastPath)) {
       const float ns = (attr & BDL_ATTR_HEAD) ? a.ns1 : a.ns0;
       if (attr & BDL_ATTR_PRIOR)
-        acc = sqnorm_fast<NOISE, RECIP, true>(a, c, gb, ns, acc);
+        acc = sqnorm_fast<NOISE, RECIP, true>(a, c, gb, ns, acc, run_grad(a, r));
       else
-        acc = sqnorm_fast<NOISE, RECIP, false>(a, c, gb, ns, acc);
+        acc = sqnorm_fast<NOISE, RECIP, false>(a, c, gb, ns, acc, run_grad(a, r));
     } else {
       for (int u = 0; u < 2; ++u) {
         const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
         if (gi >= gend) continue;
         const int64_t e = gi * 4;
         const f4v z = {0.f, 0.f, 0.f, 0.f};
-        const f4v th = ld4(a.theta, e, a.n), g = ld4(a.grad, e, a.n);
+        const bool gt = a.gbase != nullptr;
+        const f4v th = ld4(a.theta, e, a.n), g = gt ? z : ld4(a.grad, e, a.n);
         const f4v t0 = ld4(a.prior_mean, e, a.n);
         f4v ep = z;
         if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, a.n);
         if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
         for (int j = 0; j < 4; ++j) {
           if (e + j >= a.n) break;
-          const uint32_t at = run_attr(find_run_lds(a.nruns, e + j));
+          const int rr = find_run_lds(a.nruns, e + j);
+          const uint32_t at = run_attr(rr);
           if (at & BDL_ATTR_SKIP) continue;  // .grad is None: not in the norm
-          float xt = th[j], xg = g[j], xv = 0.f;
+          float xt = th[j], xg = gt ? run_grad(a, rr)[e + j] : g[j], xv = 0.f;
           const float ns = (at & BDL_ATTR_HEAD) ? a.ns1 : a.ns0;
           if (at & BDL_ATTR_PRIOR)
             update_core<BDL_SGLD_GRAD, NOISE, RECIP, true, false>(a, c, 0.f, ns, xt, xg, xv, t0[j], ep[j]);
@@ -458,6 +461,28 @@ int grid_sample(int64_t ngroups) {
 
 // Validate a step descriptor, pick the kernel instance and launch it; `clip`
 // (device pointer to (norm, coef)) scales the SGLD sampler gradient when set.
+// Dynamic LDS of a step launch: the run table, plus the per-run gradient
+// bases in grad_base mode.  Both fit the 64 KiB a launch gets by default.
+size_t run_lds_bytes(const bdl_step_args* s) {
+  return (size_t)s->nruns * (sizeof(bdl_run) + (s->grad_base ? sizeof(int64_t) : 0));
+}
+
+// Shared checks of the run table and the gradient source ("what" prefixes errors).
+int check_runs_and_grad(const bdl_step_args* s, const char* what) {
+  if (!s->runs || s->nruns < 1)
+    return fail(BDL_ERR_NULL, std::string(what) + ": runs are required");
+  if (run_lds_bytes(s) > (size_t)kMaxRuns * sizeof(bdl_run))
+    return fail(BDL_ERR_RUNS, std::string(what) + ": run table exceeds 64 KiB of LDS (4096 runs, "
+                "2730 with grad_base; merge parameter groups)");
+  if (!s->grad && !s->grad_base)
+    return fail(BDL_ERR_NULL, std::string(what) + ": grad or grad_base is required");
+  if (s->grad && !aligned16(s->grad))
+    return fail(BDL_ERR_ALIGN, std::string(what) + ": grad not 16-B aligned");
+  if (s->grad_base && (reinterpret_cast<uintptr_t>(s->grad_base) & 7u))
+    return fail(BDL_ERR_ALIGN, std::string(what) + ": grad_base not 8-B aligned");
+  return BDL_OK;
+}
+
 int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   if (!s) return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: null args");
   if (s->n < 0) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: n < 0");
@@ -473,10 +498,8 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
                          s->method == BDL_SGHMC_GRAD ||
                          (s->method == BDL_SGLD && (s->flags & BDL_FLAG_MOMENTUM));
   const bool needs_prior = s->method != BDL_CSGHMC;
-  if (!s->theta || !s->grad || !s->runs || s->nruns < 1)
-    return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: theta, grad and runs are required");
-  if (s->nruns > kMaxRuns)
-    return fail(BDL_ERR_RUNS, "bdl_sgmcmc_step: more than 4096 runs (merge parameter groups)");
+  if (!s->theta) return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: theta is required");
+  if (const int rc = check_runs_and_grad(s, "bdl_sgmcmc_step")) return rc;
   if (needs_mom && !s->mom) return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: mom is required");
   if (needs_prior && !s->prior_mean)
     return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: prior_mean is required for sghmc/sgld");
@@ -486,7 +509,7 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
     return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: mom1 is required to collect");
   if (grad_only && s->collect != BDL_COLLECT_NONE)
     return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: grad-only methods cannot collect");
-  const void* ptrs[] = {s->theta, s->grad, s->mom, s->prior_mean, s->noise, s->mom1, s->mom2};
+  const void* ptrs[] = {s->theta, s->mom, s->prior_mean, s->noise, s->mom1, s->mom2};
   for (const void* p : ptrs)
     if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_sgmcmc_step: vector not 16-B aligned");
 
@@ -511,6 +534,7 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   a.mom1 = s->mom1;
   a.mom2 = s->mom2;
   a.runs = s->runs;
+  a.gbase = s->grad_base;
   a.nruns = s->nruns;
   a.flags = s->flags;
   a.n = s->n;
@@ -535,8 +559,7 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   a.inv_ca = recip_or(s->inv_collect_a, s->collect_a);
   a.inv_cb = recip_or(s->inv_collect_b, s->collect_b);
 
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kBlock), (size_t)s->nruns * sizeof(bdl_run),
-                     stream, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kBlock), run_lds_bytes(s), stream, a);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     g_last_error = std::string("bdl_sgmcmc_step: launch failed: ") + hipGetErrorString(err);
@@ -588,7 +611,7 @@ int bdl_build_runs(const bdl_segment* segs, int32_t nseg, int64_t n, bdl_run* ou
     if (s.offset < pos || s.numel < 0 || s.offset + s.numel > n)
       return fail(BDL_ERR_RUNS, "bdl_build_runs: segments overlap, are unsorted or exceed n");
     if (!push(s.offset, BDL_ATTR_SKIP)) return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
-    if (!push(s.offset + s.numel, s.attr & 7u))
+    if (!push(s.offset + s.numel, s.attr & 0xFu))
       return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
   }
   if (!push(n, BDL_ATTR_SKIP)) return fail(BDL_ERR_ARG, "bdl_build_runs: too many runs");
@@ -624,10 +647,9 @@ int bdl_sgld_step_clipped(const bdl_step_args* s, float max_norm, void* workspac
   if (s->n == 0) return BDL_OK;
   if (s->noise_mode < BDL_NOISE_NONE || s->noise_mode > BDL_NOISE_PHILOX)
     return fail(BDL_ERR_ARG, "bdl_sgld_step_clipped: unknown noise mode");
-  if (!s->theta || !s->grad || !s->runs || !s->prior_mean || s->nruns < 1)
-    return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: theta, grad, prior_mean and runs are required");
-  if (s->nruns > kMaxRuns)
-    return fail(BDL_ERR_RUNS, "bdl_sgld_step_clipped: more than 4096 runs (merge parameter groups)");
+  if (!s->theta || !s->prior_mean)
+    return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: theta and prior_mean are required");
+  if (const int rc = check_runs_and_grad(s, "bdl_sgld_step_clipped")) return rc;
   if (s->noise_mode == BDL_NOISE_BUFFER && !s->noise)
     return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: noise buffer is required");
   hipStream_t st = (hipStream_t)stream;
@@ -640,6 +662,7 @@ int bdl_sgld_step_clipped(const bdl_step_args* s, float max_norm, void* workspac
   a.prior_mean = s->prior_mean;
   a.noise = s->noise;
   a.runs = s->runs;
+  a.gbase = s->grad_base;
   a.nruns = s->nruns;
   a.flags = s->flags;
   a.n = s->n;
@@ -656,7 +679,7 @@ int bdl_sgld_step_clipped(const bdl_step_args* s, float max_norm, void* workspac
   const int64_t iters = (ngroups + 2 * kBlock - 1) / (2 * kBlock);
   const int64_t cap = std::min<int64_t>((int64_t)device_cu_count() * g_blocks_per_cu, kMaxNormPartials);
   const int grid = (int)std::max<int64_t>(1, std::min(iters, cap));
-  const size_t shmem = (size_t)s->nruns * sizeof(bdl_run);
+  const size_t shmem = run_lds_bytes(s);
   switch (s->noise_mode) {
     case BDL_NOISE_NONE:
       hipLaunchKernelGGL(bdl_sqnorm_kernel<BDL_NOISE_NONE>, dim3(grid), dim3(kBlock), shmem, st, a, partials);
@@ -688,11 +711,9 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
   if (s->n < 0) return fail(BDL_ERR_ARG, "bdl_adam_step: n < 0");
   if (s->n == 0) return BDL_OK;
   const bool grad_only = s->method == BDL_ADAM_SGHMC_GRAD;
-  if (!s->theta || !s->grad || !s->mom || !s->prior_mean || !ad->adam_m || !ad->adam_v ||
-      !s->runs || s->nruns < 1)
-    return fail(BDL_ERR_NULL, "bdl_adam_step: theta, grad, mom, prior_mean, adam_m, adam_v and runs are required");
-  if (s->nruns > kMaxRuns)
-    return fail(BDL_ERR_RUNS, "bdl_adam_step: more than 4096 runs (merge parameter groups)");
+  if (!s->theta || !s->mom || !s->prior_mean || !ad->adam_m || !ad->adam_v)
+    return fail(BDL_ERR_NULL, "bdl_adam_step: theta, mom, prior_mean, adam_m and adam_v are required");
+  if (const int rc = check_runs_and_grad(s, "bdl_adam_step")) return rc;
   if (!grad_only && (s->flags & BDL_FLAG_MOMENTUM) && !ad->sgd_buf)
     return fail(BDL_ERR_NULL, "bdl_adam_step: sgd_buf is required with BDL_FLAG_MOMENTUM");
   if (s->noise_mode == BDL_NOISE_BUFFER && !s->noise)
@@ -701,7 +722,7 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
     return fail(BDL_ERR_NULL, "bdl_adam_step: mom1 is required to collect");
   if (s->flags & BDL_FLAG_GRAD_READY)
     return fail(BDL_ERR_ARG, "bdl_adam_step: GRAD_READY is not an Adam flag (use bdl_sgmcmc_step)");
-  const void* ptrs[] = {s->theta, s->grad, s->mom, s->prior_mean, s->noise, s->mom1, s->mom2,
+  const void* ptrs[] = {s->theta, s->mom, s->prior_mean, s->noise, s->mom1, s->mom2,
                         ad->adam_m, ad->adam_v, ad->sgd_buf};
   for (const void* p : ptrs)
     if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_adam_step: vector not 16-B aligned");
@@ -718,6 +739,7 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
   a.mom1 = s->mom1;
   a.mom2 = s->mom2;
   a.runs = s->runs;
+  a.gbase = s->grad_base;
   a.nruns = s->nruns;
   a.flags = (s->flags & ~kFlagGradIsMom) | (ad->grad_is_mom ? kFlagGradIsMom : 0);
   a.n = s->n;
@@ -757,8 +779,7 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
   const int64_t iters = (ngroups + per_iter - 1) / per_iter;
   const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
   const int grid = (int)std::max<int64_t>(1, std::min(iters, cap));
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), (size_t)s->nruns * sizeof(bdl_run),
-                     (hipStream_t)stream, a);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), run_lds_bytes(s), (hipStream_t)stream, a);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     g_last_error = std::string("bdl_adam_step: launch failed: ") + hipGetErrorString(err);

@@ -149,6 +149,7 @@ struct KArgs {
   float* __restrict__ mom1;
   float* __restrict__ mom2;
   const bdl_run* __restrict__ runs;
+  const int64_t* __restrict__ gbase;  // per-run gradient bases (grad_base mode) or null
   int32_t nruns;
   int32_t flags;
   int64_t n;
@@ -193,6 +194,31 @@ extern __shared__ bdl_run s_runs[];
 
 __device__ __forceinline__ int64_t run_end(int r) { return s_runs[r].end; }
 __device__ __forceinline__ uint32_t run_attr(int r) { return s_runs[r].attr; }
+
+// grad_base mode: the per-run gradient bases live in LDS right after the runs.
+__device__ __forceinline__ int64_t* lds_gbase(int nruns) {
+  return reinterpret_cast<int64_t*>(s_runs + nruns);
+}
+
+// Stage the run table (and the gradient bases) in LDS; dynamic LDS bytes =
+// nruns * (sizeof(bdl_run) + (gbase ? 8 : 0)), see run_lds_bytes.
+__device__ __forceinline__ void stage_runs(const KArgs& a) {
+  for (int i = threadIdx.x; i < a.nruns; i += kBlock) s_runs[i] = a.runs[i];
+  if (a.gbase) {
+    int64_t* g = lds_gbase(a.nruns);
+    for (int i = threadIdx.x; i < a.nruns; i += kBlock) g[i] = a.gbase[i];
+  }
+  __syncthreads();
+}
+
+// Where run r's gradient lives: the flat vector, or its own tensor.
+__device__ __forceinline__ float* run_grad(const KArgs& a, int r) {
+  return a.gbase ? reinterpret_cast<float*>(lds_gbase(a.nruns)[r]) : a.grad;
+}
+
+// A block iteration may take the fast path only inside one run whose
+// gradient is 16-B addressable.
+constexpr uint32_t kNoFastPath = BDL_ATTR_SKIP | BDL_ATTR_GUNALIGNED;
 
 // First run whose end is > idx.
 __device__ __forceinline__ int find_run_lds(int nruns, int64_t idx) {
@@ -321,7 +347,7 @@ struct StepTraits {
 // no branch inside, no bounds checks, every load issued before any arithmetic.
 template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL, bool PRIOR, bool GR>
 __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, int64_t gb,
-                                           float eta, float ns) {
+                                           float eta, float ns, float* gp) {
   using T = StepTraits<METHOD, COLLECT>;
   constexpr bool kPriorLoad = T::kReadPrior && PRIOR && !GR;
   f4v th[UNROLL], g[UNROLL], v[UNROLL], t0[UNROLL], ep[UNROLL], m1[UNROLL], m2[UNROLL];
@@ -331,7 +357,7 @@ __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, i
     const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
     v[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
     th[u] = vload(a.theta + e);
-    g[u] = vload(a.grad + e);
+    g[u] = vload(gp + e);
     if constexpr (T::kMom) v[u] = vload(a.mom + e);
     if constexpr (METHOD == BDL_SGLD) {
       if (c.sgd_mom_read) v[u] = vload(a.mom + e);
@@ -361,7 +387,7 @@ __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, i
       m2[u][j] = x2;
     }
     if constexpr (T::kWriteTheta) vstore(a.theta + e, th[u]);
-    if constexpr (T::kWriteGrad) vstore(a.grad + e, g[u]);
+    if constexpr (T::kWriteGrad) vstore(gp + e, g[u]);
     if constexpr (T::kMom) vstore(a.mom + e, v[u]);
     if constexpr (METHOD == BDL_SGLD) {
       if (c.sgd_mom) vstore(a.mom + e, v[u]);
@@ -375,23 +401,23 @@ __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, i
 
 template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
 __device__ __forceinline__ void chunk_fast_dispatch(const KArgs& a, const StepConst& c,
-                                                    int64_t gb, uint32_t attr) {
+                                                    int64_t gb, uint32_t attr, float* gp) {
   const bool head = (attr & BDL_ATTR_HEAD) != 0;
   const float eta = head ? a.lr1 : a.lr0;
   const float ns = head ? a.ns1 : a.ns0;
   if constexpr (METHOD == BDL_CSGHMC) {
-    chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(a, c, gb, eta, ns);
+    chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(a, c, gb, eta, ns, gp);
   } else {
     if constexpr (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) {
       if (c.grad_ready) {
-        chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, true>(a, c, gb, eta, ns);
+        chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, true>(a, c, gb, eta, ns, gp);
         return;
       }
     }
     if (attr & BDL_ATTR_PRIOR)
-      chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, true, false>(a, c, gb, eta, ns);
+      chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, true, false>(a, c, gb, eta, ns, gp);
     else
-      chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(a, c, gb, eta, ns);
+      chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(a, c, gb, eta, ns, gp);
   }
 }
 
@@ -431,7 +457,9 @@ __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, i
     if (gi >= gend) continue;
     const int64_t e = gi * 4;
     const f4v z = {0.f, 0.f, 0.f, 0.f};
-    f4v th = ld4(a.theta, e, n), g = ld4(a.grad, e, n), v = z, t0 = z, ep = z, m1 = z, m2 = z;
+    const bool gt = a.gbase != nullptr;  // gradient per tensor: element-wise below
+    f4v th = ld4(a.theta, e, n), g = gt ? z : ld4(a.grad, e, n), v = z, t0 = z, ep = z, m1 = z,
+        m2 = z;
     if (T::kMom || (METHOD == BDL_SGLD && c.sgd_mom_read)) v = ld4(a.mom, e, n);
     if (T::kReadPrior) t0 = ld4(a.prior_mean, e, n);
     if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, n);
@@ -443,9 +471,13 @@ __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, i
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (e + j >= n) break;
-      const uint32_t at = run_attr(find_run_lds(a.nruns, e + j));
+      const int rr = find_run_lds(a.nruns, e + j);
+      const uint32_t at = run_attr(rr);
+      float* gpr = gt ? run_grad(a, rr) : nullptr;
+      if (gt && !(at & BDL_ATTR_SKIP)) g[j] = gpr[e + j];
       float xt = th[j], xg = g[j], xv = v[j], x1 = m1[j], x2 = m2[j];
       update_elem<METHOD, NOISE, COLLECT, RECIP>(a, c, at, xt, xg, xv, t0[j], ep[j], x1, x2);
+      if (T::kWriteGrad && gt && !(at & BDL_ATTR_SKIP)) gpr[e + j] = xg;
       th[j] = xt;
       g[j] = xg;
       v[j] = xv;
@@ -453,7 +485,7 @@ __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, i
       m2[j] = x2;
     }
     if (T::kWriteTheta) st4(a.theta, e, n, th);
-    if (T::kWriteGrad) st4(a.grad, e, n, g);
+    if (T::kWriteGrad && !gt) st4(a.grad, e, n, g);
     if (T::kMom || (METHOD == BDL_SGLD && c.sgd_mom)) st4(a.mom, e, n, v);
     if (T::kCollect) {
       st4(a.mom1, e, n, m1);
@@ -494,9 +526,8 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
     gstep = (int64_t)gridDim.x * kIter;
   }
 
-  // stage the run table in LDS
-  for (int i = threadIdx.x; i < a.nruns; i += kBlock) s_runs[i] = a.runs[i];
-  __syncthreads();
+  // stage the run table (and gradient bases) in LDS
+  stage_runs(a);
   if (g0 >= g1) return;
 
   int r = find_run_lds(a.nruns, g0 * 4);
@@ -505,8 +536,8 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
     const int64_t gend = min(gb + kIter, g1);
     const uint32_t attr = run_attr(r);
     if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 &&
-        !(attr & BDL_ATTR_SKIP))
-      chunk_fast_dispatch<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, attr);
+        !(attr & kNoFastPath))
+      chunk_fast_dispatch<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, attr, run_grad(a, r));
     else
       chunk_slow<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, gend);
   }
@@ -572,7 +603,7 @@ __device__ __forceinline__ void adam_core(const KArgs& a, const AdamConst& c, fl
 
 template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, bool PRIOR, int U>
 __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, int64_t gb,
-                                          float eta) {
+                                          float eta, float* gp) {
   constexpr bool kReadMoments = (COLLECT == BDL_COLLECT_MEAN);
   const f4v z = {0.f, 0.f, 0.f, 0.f};
   f4v th[U], g[U], vm[U], m[U], v[U], buf[U], t0[U], ep[U], m1[U], m2[U];
@@ -581,7 +612,7 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
     const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
     buf[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
     th[u] = vload(a.theta + e);
-    g[u] = vload(a.grad + e);
+    g[u] = vload(gp + e);
     vm[u] = vload(a.mom + e);
     m[u] = vload(a.adam_m + e);
     v[u] = vload(a.adam_v + e);
@@ -618,7 +649,7 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
       m2[u][j] = x2;
     }
     if constexpr (GRADONLY)
-      vstore(a.grad + e, g[u]);
+      vstore(gp + e, g[u]);
     else
       vstore(a.theta + e, th[u]);
     vstore(a.mom + e, vm[u]);
@@ -644,7 +675,8 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
     if (gi >= gend) continue;
     const int64_t e = gi * 4;
-    f4v th = ld4(a.theta, e, n), g = ld4(a.grad, e, n), vm = ld4(a.mom, e, n);
+    const bool gt = a.gbase != nullptr;  // gradient per tensor: element-wise below
+    f4v th = ld4(a.theta, e, n), g = gt ? z : ld4(a.grad, e, n), vm = ld4(a.mom, e, n);
     f4v m = ld4(a.adam_m, e, n), v = ld4(a.adam_v, e, n), t0 = ld4(a.prior_mean, e, n);
     f4v buf = z, ep = z, m1 = z, m2 = z;
     if (!GRADONLY && c.sgd_mom_read) buf = ld4(a.sgd_buf, e, n);
@@ -656,7 +688,10 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
     }
     for (int j = 0; j < 4; ++j) {
       if (e + j >= n) break;
-      const uint32_t at = run_attr(find_run_lds(a.nruns, e + j));
+      const int rr = find_run_lds(a.nruns, e + j);
+      const uint32_t at = run_attr(rr);
+      float* gpr = gt ? run_grad(a, rr) : nullptr;
+      if (gt && !(at & BDL_ATTR_SKIP)) g[j] = gpr[e + j];
       float xt = th[j], xg = g[j], xvm = vm[j], xm = m[j], xv = v[j], xb = buf[j];
       float x1 = m1[j], x2 = m2[j];
       if (!(at & BDL_ATTR_SKIP)) {
@@ -667,6 +702,7 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
           adam_core<NOISE, RECIP, false, GRADONLY>(a, c, eta, xt, xg, xvm, xm, xv, xb, t0[j], ep[j]);
       }
       collect_core<COLLECT, RECIP>(a, cc, xt, x1, x2);
+      if (GRADONLY && gt && !(at & BDL_ATTR_SKIP)) gpr[e + j] = xg;
       th[j] = xt;
       g[j] = xg;
       vm[j] = xvm;
@@ -676,10 +712,11 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
       m1[j] = x1;
       m2[j] = x2;
     }
-    if (GRADONLY)
-      st4(a.grad, e, n, g);
-    else
+    if (GRADONLY) {
+      if (!gt) st4(a.grad, e, n, g);
+    } else {
       st4(a.theta, e, n, th);
+    }
     st4(a.mom, e, n, vm);
     st4(a.adam_m, e, n, m);
     st4(a.adam_v, e, n, v);
@@ -707,19 +744,18 @@ __device__ __forceinline__ void adam_body(const KArgs& a) {
   c.inv_cb = a.inv_cb;
   constexpr int64_t kIter = (int64_t)kBlock * U;
   const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
-  for (int i = threadIdx.x; i < a.nruns; i += kBlock) s_runs[i] = a.runs[i];
-  __syncthreads();
+  stage_runs(a);
   int r = find_run_lds(a.nruns, (int64_t)blockIdx.x * kIter * 4);
   for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {
     while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
     const int64_t gend = min(gb + kIter, ngroups);
     const uint32_t attr = run_attr(r);
-    if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 && !(attr & BDL_ATTR_SKIP)) {
+    if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 && !(attr & kNoFastPath)) {
       const float eta = (attr & BDL_ATTR_HEAD) ? a.lr1 : a.lr0;
       if (attr & BDL_ATTR_PRIOR)
-        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, true, U>(a, c, gb, eta);
+        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, true, U>(a, c, gb, eta, run_grad(a, r));
       else
-        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, false, U>(a, c, gb, eta);
+        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, false, U>(a, c, gb, eta, run_grad(a, r));
     } else {
       adam_slow<NOISE, COLLECT, RECIP, GRADONLY, U>(a, c, gb, gend);
     }

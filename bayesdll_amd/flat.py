@@ -9,8 +9,15 @@ of them exactly once per step:
 
     theta  — the network's parameters; every nn.Parameter's .data is rebound
              to a view into it, so the network computes with it directly.
-    grad   — every parameter's .grad is a view into it; autograd accumulates
-             in place (the Model zeroes it instead of net.zero_grad()).
+    grad   — gradients.  Default ("tensor" mode): NOT a flat vector — .grad is
+             set to None before backward, autograd's AccumulateGrad steals each
+             fresh gradient tensor (as after the reference's net.zero_grad()),
+             and the kernel reads every tensor's gradient where autograd left it
+             through a per-run base-address table (bdl_step_args.grad_base):
+             no zero-fill, no accumulation pass, no copy.  "flat" mode
+             (BDL_GRAD_MODE=flat, and the segment-only states of the bench and
+             kernel tests): every .grad is a view into one flat vector that
+             autograd accumulates into (zeroed before backward).
     mom    — cSGHMC/SGHMC momentum v, or the SGD momentum buffer (sgld/csgld).
     prior  — theta0 = net0's parameters (sgld/sghmc prior mean).
     noise  — only in "torch" noise mode: per-tensor torch normal_ draws.
@@ -134,12 +141,25 @@ def placed_vectors(n, device, names, method, candidates=None):
                     "method": method}
 
 
+GRAD_MODES = ("tensor", "flat")
+GRAD_TABLE_CACHE = 8  # device run/base tables kept per state (one per pointer set)
+
+
+def default_grad_mode():
+    import os
+    m = os.environ.get("BDL_GRAD_MODE", "tensor")
+    if m not in GRAD_MODES:
+        raise ValueError(f"BDL_GRAD_MODE must be one of {GRAD_MODES}, got {m!r}")
+    return m
+
+
 class FlatState:
-    """Flat buffers for one chain, bound to `net`'s parameters and grads."""
+    """Flat buffers for one chain, bound to `net`'s parameters (and, in "flat"
+    gradient mode, grads)."""
 
     def __init__(self, net, net0=None, *, readout_name=None, bias="informative",
                  need_prior=False, need_mom=True, need_noise=False, placement=None,
-                 extra=()):
+                 extra=(), grad_mode=None):
         named = list(net.named_parameters())
         if not named:
             raise ValueError("bayesdll_amd: the network has no parameters")
@@ -159,12 +179,18 @@ class FlatState:
             net, "readout_name", None)
         self.bias = bias
         self.requires_grad = [p.requires_grad for p in self.params]
+        self.grad_mode = grad_mode or default_grad_mode()
+        if self.grad_mode not in GRAD_MODES:
+            raise ValueError(f"grad_mode must be one of {GRAD_MODES}")
 
         # the swept vectors, placed (see placed_vectors) when `placement` names
-        # the sampler's kernel family
+        # the sampler's kernel family (in "tensor" mode the timing uses a
+        # scratch gradient vector, freed after the choice)
         names_ = ["theta", "grad"] + (["mom"] if need_mom else []) + \
             (["prior"] if need_prior else []) + list(extra)
         vecs, self.placement_info = placed_vectors(self.n, dev, names_, placement)
+        if self.grad_mode == "tensor":
+            del vecs["grad"]
         # further per-element state of the sampler (e.g. Adam's m, v and the
         # SGD buffer), placed together with the swept vectors, zeroed
         self.extra = {nm: vecs[nm].zero_() for nm in extra}
@@ -175,7 +201,8 @@ class FlatState:
             for p, o, k in zip(self.params, self.offsets, self.numels):
                 self.theta[o:o + k].copy_(p.data.reshape(-1))
                 p.data = self.theta[o:o + k].view(p.shape)
-        self.grad = vecs["grad"].zero_()
+        self.grad = vecs["grad"].zero_() if self.grad_mode == "flat" else None
+        self.gbase = None  # device per-run gradient bases ("tensor" mode)
         self._bind_grads()
 
         self.mom = vecs["mom"].zero_() if need_mom else None
@@ -197,12 +224,17 @@ class FlatState:
         self.nruns = int(self.runs.shape[0])
         self._base_runs = (self.runs, self.nruns)
         self._skip_tables = {}
+        self._grad_tables = {}
+        self._untouched = ()
         # which parameters received a gradient in the current backward: the
         # reference skips a parameter whose .grad is None after net.zero_grad()
-        # + backward (`if p.grad is not None`, e.g. methods/csghmc.py:749)
-        self._touched = [False] * len(self.params)
+        # + backward (`if p.grad is not None`, e.g. methods/csghmc.py:749).
+        # "tensor" mode sees it directly (.grad stays None); "flat" mode marks
+        # it with a post-accumulate hook (its .grad views always exist).
+        self._touched = [False] * len(self.params) if self.grad_mode == "flat" else []
         self._hooks = [p.register_post_accumulate_grad_hook(self._mark(i))
-                       for i, p in enumerate(self.params) if p.requires_grad]
+                       for i, p in enumerate(self.params) if p.requires_grad] \
+            if self.grad_mode == "flat" else []
 
     def _mark(self, i):
         touched = self._touched
@@ -236,6 +268,10 @@ class FlatState:
             self.n, self.device, names_, placement if init is None else None)
         self.extra = {nm: vecs[nm].zero_() for nm in extra}
         self.theta = vecs["theta"] if init is None else init
+        self.grad_mode = "flat"
+        self.gbase = None
+        self._grad_tables = {}
+        self._untouched = ()
         self.grad = vecs["grad"].zero_()
         self.mom = vecs["mom"].zero_() if need_mom else None
         self.prior = vecs["prior"].zero_() if need_prior else None
@@ -251,6 +287,11 @@ class FlatState:
 
     # ---------------------------------------------------------------- grads
     def _bind_grads(self):
+        if self.grad_mode == "tensor":
+            for p in self.params:
+                p.grad = None
+            self._grad_ptrs = [0 if rg else None for rg in self.requires_grad]
+            return
         self._grad_ptrs = []
         for p, o, k, rg in zip(self.params, self.offsets, self.numels,
                                [p.requires_grad for p in self.params]):
@@ -261,7 +302,14 @@ class FlatState:
                 self._grad_ptrs.append(None)
 
     def zero_grad(self):
-        """Replaces net.zero_grad(): keep .grad bound to the flat buffer."""
+        """Replaces net.zero_grad().  "tensor" mode: .grad = None (torch's
+        set_to_none), so backward hands each fresh gradient tensor over without
+        an accumulation kernel.  "flat" mode: zero the flat buffer and keep
+        every .grad bound to it."""
+        if self.grad_mode == "tensor":
+            for p in self.params:
+                p.grad = None
+            return
         self.grad.zero_()
         for i in range(len(self._touched)):
             self._touched[i] = False
@@ -274,7 +322,12 @@ class FlatState:
         """After backward: if user code replaced a .grad, copy it into the flat
         buffer; then select the run table of this step — parameters that got no
         gradient (unused in the forward pass, or .grad set to None) are
-        skipped, exactly like the reference's `if p.grad is not None`."""
+        skipped, exactly like the reference's `if p.grad is not None`.
+        "tensor" mode: select (or build) the run / gradient-base table of the
+        gradient tensors autograd produced."""
+        if self.grad_mode == "tensor":
+            self._sync_tensor_grads()
+            return
         rebind = False
         untouched = []
         for i, (p, o, k, ptr) in enumerate(zip(self.params, self.offsets, self.numels,
@@ -309,10 +362,62 @@ class FlatState:
             tab = self._skip_tables[untouched] = (runs, int(runs.shape[0]))
         self.runs, self.nruns = tab
 
+    def _sync_tensor_grads(self):
+        ptrs, untouched = [], []
+        for i, (p, rg) in enumerate(zip(self.params, self.requires_grad)):
+            g = p.grad if rg else None
+            if g is None:
+                ptrs.append(0)
+                if rg:
+                    untouched.append(i)
+                continue
+            if g.dtype != torch.float32 or g.device != self.device or not g.is_contiguous():
+                g = g.to(device=self.device, dtype=torch.float32).contiguous()
+                p.grad = g
+            ptrs.append(g.data_ptr())
+        key = tuple(ptrs)
+        tab = self._grad_tables.get(key)
+        if tab is None:
+            tab = self._build_grad_table(ptrs)
+            if len(self._grad_tables) >= GRAD_TABLE_CACHE:
+                self._grad_tables.pop(next(iter(self._grad_tables)))
+            self._grad_tables[key] = tab
+        self.use_grad_table((tab[0], tab[1], tab[2], tuple(untouched)))
+
+    def _build_grad_table(self, ptrs):
+        """One run per tensor (a run must not span two gradient tensors): end,
+        attributes (+SKIP without a gradient, +GUNALIGNED when the tensor's
+        base address minus 4*offset is not 16-B aligned), and the base
+        address; packed as [runs (2 int64 each) | bases] in one device
+        tensor, copied from pinned memory on the current stream."""
+        nt = len(self.params)
+        host = torch.empty(3 * nt, dtype=torch.int64).pin_memory()
+        h = host.numpy()
+        for i, (o, k, a, ptr) in enumerate(zip(self.offsets, self.numels, self.attrs, ptrs)):
+            base = ptr - 4 * o if ptr else 0
+            at = a | (L.ATTR_SKIP if not ptr else 0)
+            if ptr and base % 16:
+                at |= L.ATTR_GUNALIGNED
+            h[2 * i] = o + k
+            h[2 * i + 1] = at
+            h[2 * nt + i] = base
+        dev = host.to(self.device, non_blocking=True)
+        return dev[:2 * nt].view(nt, 2), nt, dev[2 * nt:]
+
+    def grad_table(self):
+        """The run / gradient-base selection of the current step (to reuse
+        when the same gradient tensors are produced again, e.g. graph replay)."""
+        return (self.runs, self.nruns, self.gbase, self._untouched)
+
+    def use_grad_table(self, t):
+        self.runs, self.nruns, self.gbase, self._untouched = t
+
     def has_grad(self, i):
         """Did parameter i receive a gradient in the current step?"""
         if not self.requires_grad[i]:
             return False
+        if self.grad_mode == "tensor":
+            return i not in self._untouched
         return not self._touched or self._touched[i]
 
     def check_bound(self):

@@ -41,7 +41,10 @@ def _step_args(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1
                mom_buf=None):
     a = L.StepArgs()
     a.theta = state.theta.data_ptr()
-    a.grad = state.grad.data_ptr()
+    g = getattr(state, "grad", None)
+    a.grad = None if g is None else g.data_ptr()
+    gb = getattr(state, "gbase", None)  # per-tensor gradients ("tensor" grad mode)
+    a.grad_base = None if gb is None else gb.data_ptr()
     mb = state.mom if mom_buf is None else mom_buf  # mom_buf: a separate SGD buffer
     a.mom = None if mb is None else mb.data_ptr()
     a.prior_mean = None if state.prior is None else state.prior.data_ptr()

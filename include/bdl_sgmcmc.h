@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define BDL_ABI_VERSION 2
+#define BDL_ABI_VERSION 3
 
 typedef enum bdl_status {
   BDL_OK = 0,
@@ -103,6 +103,8 @@ typedef enum bdl_collect {
 #define BDL_ATTR_HEAD 0x1     /* readout_name in pname -> lr group 1          */
 #define BDL_ATTR_PRIOR 0x2    /* prior term applied (not an uninformative bias)*/
 #define BDL_ATTR_SKIP 0x4     /* parameter has no grad: left untouched          */
+#define BDL_ATTR_GUNALIGNED 0x8 /* grad_base mode: this run's gradient base is not
+                                 16-byte aligned (element-wise loads only)       */
 
 /* Flags for bdl_step_args.flags. */
 #define BDL_FLAG_FIRST_STEP 0x1  /* SGD momentum buffer does not exist yet: buf = grad */
@@ -166,6 +168,17 @@ typedef struct bdl_step_args {
   uint64_t seed;           /* Philox key                                            */
   uint64_t chain;          /* chain id (rank)                                        */
   uint64_t step;           /* global step counter                                    */
+  /* Gradient in place, per tensor (null: the flat `grad` vector is used).
+   * Device array of nruns byte addresses: run r's gradient for flat element i
+   * is ((float*)grad_base[r])[i], i.e. grad_base[r] = (address of the tensor's
+   * own .grad) - 4 * (flat offset of the tensor).  autograd's per-parameter
+   * gradient tensors are then read (and, for *_GRAD methods, written) where
+   * autograd left them — no flat gradient buffer, no zero-fill and no
+   * accumulation pass before the step (torch's AccumulateGrad steals the
+   * fresh gradient when .grad is None).  Runs must not span two tensors;
+   * SKIP runs may hold 0; a base that is not 16-byte aligned needs
+   * BDL_ATTR_GUNALIGNED on its run.  `grad` may be null in this mode. */
+  const int64_t* grad_base;
 } bdl_step_args;
 
 /* Extra state and scalars of the Adam-preconditioned SGHMC step.  Per element,

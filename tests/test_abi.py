@@ -158,6 +158,15 @@ def test_entry_points_validate_before_touching_the_device():
     a.grad = 0x2004
     assert h.bdl_sgmcmc_step(a, None) == -2                         # misaligned vector
     a.grad = 0x2000
+    # per-tensor gradient bases instead of the flat grad vector
+    a.grad, a.grad_base = None, None
+    assert h.bdl_sgmcmc_step(a, None) == -1                         # neither grad nor grad_base
+    assert b"grad_base" in h.bdl_last_error()
+    a.grad_base = 0x5004
+    assert h.bdl_sgmcmc_step(a, None) == -2                         # base table not 8-B aligned
+    a.grad_base, a.nruns = 0x5000, 2731
+    assert h.bdl_sgmcmc_step(a, None) == -5                         # runs + bases > 64 KiB LDS
+    a.grad, a.grad_base, a.nruns = 0x2000, None, 1
     a.method = L.SGLD
     assert h.bdl_sgmcmc_step(a, None) == -1                         # sgld needs prior_mean
     a.n = 0
