@@ -362,6 +362,28 @@ class FlatState:
             tab = self._skip_tables[untouched] = (runs, int(runs.shape[0]))
         self.runs, self.nruns = tab
 
+    def use_tensor_grads(self, grads):
+        """Segment-only states (no nn.Module): read the gradient of segment i
+        from grads[i] (a contiguous fp32 device tensor, or None = no gradient)
+        through the per-run base table, as "tensor" mode does for autograd's
+        .grad tensors; the flat gradient vector is dropped."""
+        if len(grads) != len(self.numels):
+            raise ValueError("use_tensor_grads: one gradient (or None) per segment")
+        self.grad_mode, self.grad = "tensor", None
+        ptrs, untouched = [], []
+        for i, (g, k) in enumerate(zip(grads, self.numels)):
+            if g is None:
+                ptrs.append(0)
+                untouched.append(i)
+                continue
+            if (g.dtype != torch.float32 or g.device != self.device or not g.is_contiguous()
+                    or g.numel() != k):
+                raise ValueError(f"use_tensor_grads: gradient {i} must be a contiguous fp32 "
+                                 f"tensor of {k} elements on {self.device}")
+            ptrs.append(g.data_ptr())
+        tab = self._build_grad_table(ptrs)
+        self.use_grad_table((tab[0], tab[1], tab[2], tuple(untouched)))
+
     def _sync_tensor_grads(self):
         ptrs, untouched = [], []
         for i, (p, rg) in enumerate(zip(self.params, self.requires_grad)):
@@ -390,7 +412,7 @@ class FlatState:
         base address minus 4*offset is not 16-B aligned), and the base
         address; packed as [runs (2 int64 each) | bases] in one device
         tensor, copied from pinned memory on the current stream."""
-        nt = len(self.params)
+        nt = len(self.numels)
         host = torch.empty(3 * nt, dtype=torch.int64).pin_memory()
         h = host.numpy()
         for i, (o, k, a, ptr) in enumerate(zip(self.offsets, self.numels, self.attrs, ptrs)):

@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--grid-stride", type=int, default=-1)
     ap.add_argument("--no-autotune", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=10)
+    ap.add_argument("--grad-mode", default="flat", choices=["flat", "tensor"],
+                    help="gradient source of the timed step: one flat vector, or one tensor "
+                         "per parameter read through the per-run base table (the product's "
+                         "default with autograd)")
     ap.add_argument("--no-aux", action="store_true",
                     help="skip the posterior-sample / moments sweeps after the timed region")
     ap.add_argument("--prewarm-seconds", type=float, default=0.0,
@@ -285,6 +289,10 @@ def main():
         st.theta.normal_(0.0, 0.02, generator=gen)
     st.grad.normal_(0.0, 1e-3, generator=gen)
     n = st.n
+    tensor_grads = None
+    if a.grad_mode == "tensor":  # one gradient tensor per parameter, as autograd leaves them
+        tensor_grads = [st.grad[o:o + k].clone() for o, k in zip(st.offsets, st.numels)]
+        st.use_tensor_grads(tensor_grads)
 
     # config 4 hyper-parameters; config 3 for --method sgld
     lr, lr_head, alpha, nd, ND, Ninflate, prior_sig = 1e-4, 1e-2, 0.18, 0.01, 1840, 1.0, 1.0
@@ -473,7 +481,8 @@ def main():
                                 f"{a.backbone} SGLD + SGD(momentum 0.5) fused update (config 3)"),
                    "params": n, "tensors": len(segs), "readout": readout,
                    "cycles": a.cycles, "thin": a.thin, "beta": 0.5, "noise": "philox",
-                   "parallelism": f"{world} independent chains (1/GPU)"},
+                   "parallelism": f"{world} independent chains (1/GPU)",
+                   "grad_mode": a.grad_mode},
         "hbm_gbs": round(hbm_gbs * world, 1),
         "eval_collective": collective,
         "launch": launch,
