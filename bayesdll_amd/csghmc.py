@@ -157,6 +157,7 @@ class Runner:
         args, logger = self.args, self.logger
         self.net.train()
         loss, error, nb_samples = 0, 0, 0
+        errs = []
         cycle_updated = False
         bpe = len(train_loader)
         sched = self.cyclical_scheduler
@@ -187,7 +188,7 @@ class Runner:
             pred = out.data.max(dim=1)[1]
             err = pred.ne(y.data).sum()
             loss += loss_ * len(y)
-            error += err.item()
+            errs.append(err)  # summed once per epoch: no second host sync per step
             nb_samples += len(y)
 
             if should_sample:
@@ -214,6 +215,7 @@ class Runner:
                     with torch.no_grad():
                         self.save_ckpt(epoch=sched.current_epoch)
                     self._cycle_completed(cycle_number)
+        error = int(torch.stack(errs).sum().item()) if errs else 0
         return loss / nb_samples, error / nb_samples, cycle_updated
 
     def _cycle_completed(self, cycle_number):

@@ -168,6 +168,7 @@ class Runner:
         args, logger = self.args, self.logger
         self.net.train()
         loss, error, nb = 0, 0, 0
+        errs = []
         for x, y in train_loader:
             x, y = x.to(args.device), y.to(args.device)
             do_collect = collect and (bi + 1) % self.thin == 0
@@ -182,12 +183,13 @@ class Runner:
             pred = out.data.max(dim=1)[1]
             err = pred.ne(y.data).sum()
             loss += loss_ * len(y)
-            error += err.item()
+            errs.append(err)  # summed once per epoch: no second host sync per step
             nb += len(y)
             bi += 1
             if do_collect:
                 logger.info("(post-burnin) accumulate posterior samples")
                 self.post_theta_cnt += 1
+        error = int(torch.stack(errs).sum().item()) if errs else 0
         return loss / nb, error / nb, bi
 
     # --------------------------------------------------------------- evaluate
