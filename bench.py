@@ -446,6 +446,7 @@ def main():
         gbs = BYTES_PER_ELEM[kind] * n / (avg * 1e-3) / 1e9
         table[kind] = {"launches": kinds.count(kind), "timed": len(ms), "avg_ms": round(avg, 4),
                        "p10_ms": round(float(np.percentile(ms, 10)), 4),
+                       "p50_ms": round(float(np.percentile(ms, 50)), 4),
                        "p90_ms": round(float(np.percentile(ms, 90)), 4),
                        "bytes_per_elem": BYTES_PER_ELEM[kind], "gbs": round(gbs, 1)}
     dominant = max(table, key=lambda k: table[k]["launches"] * table[k]["avg_ms"])
