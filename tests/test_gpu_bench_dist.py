@@ -50,3 +50,32 @@ def test_bench_two_ranks_gloo():
     assert ec["backend"] == "gloo" and ec["finite"] is True
     assert "cpu_baseline" not in d  # rank 0 at N=1 only
     assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
+
+
+def test_rccl_process_group_init_as_bench_does():
+    """The RCCL ("nccl") process-group calls bench.py's N-GPU path makes —
+    init_process_group with device_id, barrier, all_reduce(MAX) of the timing,
+    the chains collectives on device tensors — in a one-rank group on the box's
+    GPU (several ranks need one GPU each)."""
+    code = r'''
+import os, torch, torch.distributed as dist
+from bayesdll_amd import chains
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+dist.barrier()
+t = torch.tensor([1.5], dtype=torch.float64, device="cuda")
+dist.all_reduce(t, op=dist.ReduceOp.MAX)
+x = torch.ones(1 << 20, device="cuda")
+dist.all_reduce(x)
+lp = torch.log_softmax(torch.randn(8, 10, device="cuda"), 1)
+assert torch.equal(chains.average_predictive(lp), lp)
+torch.cuda.synchronize()
+print("RCCL_OK", dist.get_backend(), float(t.item()), float(x[0].item()))
+dist.destroy_process_group()
+'''
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()), PYTHONPATH=ROOT)
+    p = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True,
+                       text=True, timeout=180)
+    assert p.returncode == 0, (p.stdout + p.stderr)[-3000:]
+    assert "RCCL_OK nccl 1.5 1.0" in p.stdout
