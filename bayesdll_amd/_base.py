@@ -126,6 +126,9 @@ class FusedModelBase(nn.Module):
             if len(self._graphs) >= MAX_GRAPHS:
                 return None
             g = self._capture(st, net, x, y, criterion)
+            if g is None:  # not capturable as is: stay eager for this shape
+                self.graph = False
+                return None
             self._graphs[key] = g
         if any(p.grad is not gt for p, gt in zip(st.params, g["grads"])):
             self._graphs.clear()    # user code re-bound .grad: recapture on the next step
@@ -164,6 +167,10 @@ class FusedModelBase(nn.Module):
             out = net(sx)
             loss = criterion(out, sy)
             loss.backward()
+        if st.grad is None and any(p.grad is not None and (p.grad.dtype != torch.float32 or
+                                                           not p.grad.is_contiguous())
+                                   for p in st.params):
+            return None  # the table would point at eager copies, not the graph's outputs
         st.sync_grads()  # the (static) gradient tensors' table; which parameters got one
         # keep the static outputs, not the captured autograd graph: its
         # AccumulateGrad nodes would otherwise outlive the capture and meet the
