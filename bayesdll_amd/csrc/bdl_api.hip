@@ -143,6 +143,7 @@ __device__ __forceinline__ void sqnorm_body(const KArgs& a, double* __restrict__
       else
         acc = sqnorm_fast<NOISE, RECIP, false>(a, c, gb, ns, acc, run_grad(a, r));
     } else {
+      int rr = r;  // run of the chunk's first element; a lane's elements only move forward
       for (int u = 0; u < 2; ++u) {
         const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
         if (gi >= gend) continue;
@@ -156,7 +157,7 @@ __device__ __forceinline__ void sqnorm_body(const KArgs& a, double* __restrict__
         if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
         for (int j = 0; j < 4; ++j) {
           if (e + j >= a.n) break;
-          const int rr = find_run_lds(a.nruns, e + j);
+          while (rr < a.nruns - 1 && run_end(rr) <= e + j) ++rr;
           const uint32_t at = run_attr(rr);
           if (at & BDL_ATTR_SKIP) continue;  // .grad is None: not in the norm
           float xt = th[j], xg = gt ? run_grad(a, rr)[e + j] : g[j], xv = 0.f;

@@ -448,9 +448,10 @@ __device__ __forceinline__ void update_elem(const KArgs& a, const StepConst& c, 
 // O(#runs + #blocks) iterations per launch.
 template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
 __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, int64_t gb,
-                                           int64_t gend) {
+                                           int64_t gend, int r0) {
   using T = StepTraits<METHOD, COLLECT>;
   const int64_t n = a.n;
+  int rr = r0;  // run of the chunk's first element; a lane's elements only move forward
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
@@ -471,7 +472,7 @@ __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, i
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (e + j >= n) break;
-      const int rr = find_run_lds(a.nruns, e + j);
+      while (rr < a.nruns - 1 && run_end(rr) <= e + j) ++rr;
       const uint32_t at = run_attr(rr);
       float* gpr = gt ? run_grad(a, rr) : nullptr;
       if (gt && !(at & BDL_ATTR_SKIP)) g[j] = gpr[e + j];
@@ -539,7 +540,7 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
         !(attr & kNoFastPath))
       chunk_fast_dispatch<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, attr, run_grad(a, r));
     else
-      chunk_slow<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, gend);
+      chunk_slow<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, gend, r);
   }
 }
 
@@ -665,8 +666,9 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
 
 template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, int U>
 __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, int64_t gb,
-                                          int64_t gend) {
+                                          int64_t gend, int r0) {
   const int64_t n = a.n;
+  int rr = r0;  // run of the chunk's first element; a lane's elements only move forward
   const f4v z = {0.f, 0.f, 0.f, 0.f};
   StepConst cc;
   cc.inv_ca = c.inv_ca;
@@ -688,7 +690,7 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
     }
     for (int j = 0; j < 4; ++j) {
       if (e + j >= n) break;
-      const int rr = find_run_lds(a.nruns, e + j);
+      while (rr < a.nruns - 1 && run_end(rr) <= e + j) ++rr;
       const uint32_t at = run_attr(rr);
       float* gpr = gt ? run_grad(a, rr) : nullptr;
       if (gt && !(at & BDL_ATTR_SKIP)) g[j] = gpr[e + j];
@@ -757,7 +759,7 @@ __device__ __forceinline__ void adam_body(const KArgs& a) {
       else
         adam_fast<NOISE, COLLECT, RECIP, GRADONLY, false, U>(a, c, gb, eta, run_grad(a, r));
     } else {
-      adam_slow<NOISE, COLLECT, RECIP, GRADONLY, U>(a, c, gb, gend);
+      adam_slow<NOISE, COLLECT, RECIP, GRADONLY, U>(a, c, gb, gend, r);
     }
   }
 }

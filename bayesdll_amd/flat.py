@@ -256,6 +256,8 @@ class FlatState:
         self.offsets = np.concatenate([[0], np.cumsum(self.numels)[:-1]]).astype(np.int64).tolist()
         self.n = int(sum(self.numels))
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.readout_name = readout_name
         self.bias = bias
         self.requires_grad = [True] * len(self.names)
