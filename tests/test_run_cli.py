@@ -1,0 +1,52 @@
+"""bayesdll_amd.run: the reference's flag / hparams surface (demo_mnist.py)
+on CPU (parsing, split arithmetic, synthetic batches) and one tiny end-to-end
+run per sampler family on the GPU."""
+import pytest
+import torch
+
+
+def test_parse_hparams_like_demo_mnist():
+    from bayesdll_amd.run import parse_hparams
+    hp, tag = parse_hparams('"prior_sig=1.0,Ninflate=1e3,nd=1.0,burnin=5,thin=10,bias=informative"')
+    assert hp == {"prior_sig": "1.0", "Ninflate": "1e3", "nd": "1.0", "burnin": "5",
+                  "thin": "10", "bias": "informative"}          # values stay strings
+    assert tag == "prior_sig=1.0_Ninflate=1e3_nd=1.0_burnin=5_thin=10_bias=informative"
+    assert parse_hparams("")[0] == {} and parse_hparams("a=1,junk")[0] == {"a": "1"}
+
+
+def test_defaults_and_split_sizes():
+    from bayesdll_amd.run import DEFAULT_HPARAMS, METHODS, build_parser, parse_hparams, prepare
+    for m in METHODS:
+        hp, _ = parse_hparams(DEFAULT_HPARAMS[m])
+        assert {"prior_sig", "Ninflate", "nd", "burnin", "thin", "bias", "nst"} <= set(hp)
+    args = build_parser().parse_args(["--dataset", "pets", "--val_heldout", "0.5",
+                                      "--batch_size", "16", "--train_size", "40",
+                                      "--test_size", "20"])
+    tr, va, te, nd = prepare(args, torch.device("cpu"))
+    assert nd == 20 and args.num_classes == 37           # val carved from train
+    assert len(tr) == 2 and len(va) == 2 and len(te) == 2
+    xb = [x for x, _ in tr]
+    assert [tuple(x.shape) for x in xb] == [(16, 3, 224, 224), (4, 3, 224, 224)]
+    x2 = [x for x, _ in tr]
+    assert all(torch.equal(a, b) for a, b in zip(xb, x2))  # same batches every epoch
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["sgld", "csghmc", "adam_sghmc"])
+def test_cli_end_to_end_tiny(method, tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    import numpy as np
+    from bayesdll_amd.run import main
+    hp = {"sgld": "prior_sig=1.0,Ninflate=1e3,nd=1.0,burnin=1,thin=1,bias=informative,nst=2",
+          "csghmc": "prior_sig=1.0,Ninflate=1.0,nd=0.01,burnin=0,momentum_decay=0.18,thin=1,"
+                    "bias=informative,nst=2",
+          "adam_sghmc": ""}[method]  # adam_sghmc: the method's default hparams
+    res = main(["--method", method, "--dataset", "mnist", "--backbone", "mlp_mnist",
+                "--epochs", "2", "--num_cycles", "2", "--batch_size", "64", "--lr", "1e-2",
+                "--train_size", "256", "--test_size", "64", "--val_heldout", "0",
+                "--log_dir", str(tmp_path)] + (["--hparams", hp] if hp else []))
+    logs = list(tmp_path.rglob("logs.txt"))
+    assert len(logs) == 1 and logs[0].stat().st_size > 0
+    if res is not None:  # the cyclical Runners return a results dict
+        assert np.isfinite(res["losses_train"]).all()
