@@ -199,3 +199,48 @@ def test_model_steps_leave_grads_as_autograd_tensors():
         assert p.grad is not None and p.grad.data_ptr() != 0
     assert torch.equal(m_t.flat.theta, m_f.flat.theta)
     np.testing.assert_array_equal(m_t.flat.mom.cpu().numpy(), m_f.flat.mom.cpu().numpy())
+
+
+@pytest.mark.parametrize("method", ["sgld", "adam_sghmc"])
+def test_frozen_parameters_tensor_vs_flat(method):
+    """requires_grad=False parameters (a frozen first layer) are SKIP runs in
+    both gradient modes: untouched, no noise, no SGD step; the rest of the
+    chain is bit-identical between the modes."""
+    import os
+    import importlib
+    from bayesdll_amd.sgld import FusedSGD
+    from fakenet import MLP, init_vector, synthetic_mnist
+    mod = importlib.import_module(f"bayesdll_amd.{method}")
+    n = 2797010
+    init = torch.tensor(init_vector(51, n, 0.03))
+    prior = torch.tensor(init_vector(52, n, 0.03))
+    data = synthetic_mnist(53, 192, 64, device=DEV)
+    crit = torch.nn.CrossEntropyLoss()
+
+    def run(mode):
+        os.environ["BDL_GRAD_MODE"] = mode
+        try:
+            net, net0 = MLP(), MLP()
+            with torch.no_grad():
+                torch.nn.utils.vector_to_parameters(init.clone(), net.parameters())
+                torch.nn.utils.vector_to_parameters(prior.clone(), net0.parameters())
+            net, net0 = net.to(DEV), net0.to(DEV)
+            for p in net.layers[0].parameters():
+                p.requires_grad_(False)
+            if method == "sgld":
+                model = mod.Model(30000.0, prior_sig=1.0)
+            else:
+                model = mod.Model(30000.0, prior_sig=1.0, momentum_decay=0.1)
+            model.noise_mode, model.seed = "philox", 9
+            opt = torch.optim.SGD(net.parameters(), lr=1e-2, momentum=0.5)
+            fsgd = FusedSGD(opt, 0.5)
+            w0 = net.layers[0].weight.detach().clone()
+            for x, y in data:
+                model(x, y, net, net0, crit, [1e-2, 1e-2], 1.0, 0.5, sgd=fsgd)
+            torch.cuda.synchronize()
+            assert torch.equal(net.layers[0].weight.detach(), w0)
+            return model.flat.theta.clone()
+        finally:
+            os.environ.pop("BDL_GRAD_MODE", None)
+
+    assert torch.equal(run("tensor"), run("flat"))
