@@ -68,6 +68,19 @@ def chain_world():
     return chains.world()
 
 
+def bind_chain_log_dir(args):
+    """With several chains (one per rank) sharing a log_dir, every chain writes
+    its checkpoints / logits / snapshots under <log_dir>/chain<rank> (the
+    reference is single-chain, so its file names would collide).  One chain:
+    unchanged."""
+    if chains.world() > 1 and getattr(args, "log_dir", None) is not None \
+            and not getattr(args, "_chain_dir_bound", False):
+        args.log_dir = os.path.join(args.log_dir, f"chain{chains.rank()}")
+        os.makedirs(args.log_dir, exist_ok=True)
+        args._chain_dir_bound = True
+    return args
+
+
 def chain_average_logprob(logp):
     """Across-chain posterior-predictive average (bayesdll_amd.chains)."""
     return chains.average_predictive(logp)

@@ -33,7 +33,7 @@ from .cyclical import CyclicalSGMCMC
 class Runner:
 
     def __init__(self, net, net0, args, logger):
-        self.args = args
+        self.args = R.bind_chain_log_dir(args)
         self.logger = logger
         # prior backbone (zeros if not pretrained) — kept for API parity; the
         # cSGHMC update never reads it (Q1, methods/csghmc.py:759-762)

@@ -160,8 +160,7 @@ def main(argv=None):
     main_dir = (f"{args.dataset}_val_heldout{args.val_heldout}/{args.backbone}/"
                 f"{args.method}_{hpstr}_pretr{pretr}/ep{args.epochs}_bs{args.batch_size}_"
                 f"lr{args.lr}_lrh{args.lr_head}_mo{args.momentum}/seed{args.seed}_"
-                + datetime.now().strftime("%Y_%m%d_%H%M%S")
-                + (f"_chain{rank}" if world > 1 else ""))
+                + datetime.now().strftime("%Y_%m%d_%H%M%S"))
     args.log_dir = os.path.join(args.log_dir, main_dir)
     os.makedirs(args.log_dir, exist_ok=True)
     logging.basicConfig(handlers=[logging.FileHandler(os.path.join(args.log_dir, "logs.txt")),

@@ -66,7 +66,7 @@ class FusedSGD:
 class Runner:
 
     def __init__(self, net, net0, args, logger):
-        self.args = args
+        self.args = R.bind_chain_log_dir(args)
         self.logger = logger
         if args.pretrained is None:
             self.net0 = copy.deepcopy(net)

@@ -64,7 +64,8 @@ def run_chain(method, chain=None):
     runner.train(train, None, test)
     loss, err, targets, logits, logits_all = runner.evaluate(test)
     torch.cuda.synchronize()
-    return {"theta": runner.model.flat.theta.detach().cpu().numpy(),
+    return {"log_dir": np.array(runner.args.log_dir),
+            "theta": runner.model.flat.theta.detach().cpu().numpy(),
             "chain": np.int64(runner.model.chain), "loss": np.float64(loss),
             "err": np.float64(err), "targets": targets, "logits": logits,
             "logits_all": logits_all}

@@ -71,6 +71,9 @@ def test_two_chain_ensemble_matches_single_chains(method, tmp_path):
     singles = [run_chain(method, chain=r) for r in range(WORLD)]
     for r in range(WORLD):
         assert int(ranks[r]["chain"]) == r
+        # each chain writes its checkpoints / logits under <log_dir>/chain<rank>
+        assert str(ranks[r]["log_dir"]).endswith(f"chain{r}")
+        assert not str(singles[r]["log_dir"]).endswith(f"chain{r}")
         # the chain a rank samples is the single-process chain with its id, bit for bit
         np.testing.assert_array_equal(ranks[r]["theta"], singles[r]["theta"])
         np.testing.assert_array_equal(ranks[r]["logits_all"], singles[r]["logits_all"])
