@@ -68,6 +68,18 @@ def chain_world():
     return chains.world()
 
 
+def check_divergence(runner, ep):
+    """Once per epoch: did the sampler write a non-finite theta (or gradient)?
+    The step kernels raise a device flag (bdl_step_args.nonfinite) instead of
+    the host checking every step; the reference has no such guard and runs on
+    with NaNs.  Logs a warning and records the epoch in runner.diverged_epochs."""
+    st = runner.model.flat
+    if st is not None and st.diverged():
+        runner.diverged_epochs.append(ep)
+        runner.logger.warning(f"[Epoch {ep}] the sampler wrote non-finite parameters: the chain "
+                              "diverged (step size too large for the gradient scale?)")
+
+
 def bind_chain_log_dir(args):
     """With several chains (one per rank) sharing a log_dir, every chain writes
     its checkpoints / logits / snapshots under <log_dir>/chain<rank> (the

@@ -34,6 +34,7 @@ class Runner:
 
     def __init__(self, net, net0, args, logger):
         self.args = R.bind_chain_log_dir(args)
+        self.diverged_epochs = []
         self.logger = logger
         # prior backbone (zeros if not pretrained) — kept for API parity; the
         # cSGHMC update never reads it (Q1, methods/csghmc.py:759-762)
@@ -106,6 +107,7 @@ class Runner:
             self.cyclical_scheduler.current_epoch = ep
             tic = time.time()
             losses_train[ep], errors_train[ep], cycle_updated = self.train_one_epoch(train_loader)
+            R.check_divergence(self, ep)
             logger.info(f"[Epoch {ep}/{args.epochs}] Training summary: loss = "
                         f"{losses_train[ep]:.4f}, prediction error = {errors_train[ep]:.4f} "
                         f"(time: {time.time() - tic:.4f} seconds)")

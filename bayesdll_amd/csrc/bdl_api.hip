@@ -555,6 +555,7 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   a.chain = s->chain;
   a.step = s->step;
   a.clip = clip;
+  a.nonfinite = s->nonfinite;
   a.inv_s2 = recip_or(s->inv_sigma2, s->sigma2);
   a.inv_nd = recip_or(s->inv_n_data, s->n_data);
   a.inv_ca = recip_or(s->inv_collect_a, s->collect_a);
@@ -755,6 +756,7 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
   a.seed = s->seed;
   a.chain = s->chain;
   a.step = s->step;
+  a.nonfinite = s->nonfinite;
   a.adam_m = ad->adam_m;
   a.adam_v = ad->adam_v;
   a.sgd_buf = ad->sgd_buf;

@@ -158,6 +158,7 @@ struct KArgs {
   float one_minus_alpha, prior_sig, sigma2, n_data, mu, ca, cb;
   uint64_t seed, chain, step;
   const float* __restrict__ clip;  // (total_norm, coef) from the clip finalize, or null
+  int32_t* __restrict__ nonfinite;  // set to 1 if a written theta / grad value is not finite (or null)
   // Adam-preconditioned SGHMC only (bdl_adam_step)
   float* __restrict__ adam_m;
   float* __restrict__ adam_v;
@@ -219,6 +220,18 @@ __device__ __forceinline__ float* run_grad(const KArgs& a, int r) {
 // A block iteration may take the fast path only inside one run whose
 // gradient is 16-B addressable.
 constexpr uint32_t kNoFastPath = BDL_ATTR_SKIP | BDL_ATTR_GUNALIGNED;
+
+// Divergence guard: any element of the vector not finite (NaN / +-Inf)?
+__device__ __forceinline__ uint32_t nonfinite4(f4v v) {
+  return (uint32_t)(!__builtin_isfinite(v.x) | !__builtin_isfinite(v.y) |
+                    !__builtin_isfinite(v.z) | !__builtin_isfinite(v.w));
+}
+
+// End of a step launch: report divergence with one atomic per offending lane
+// (never taken on a healthy chain, so the guard costs a compare per element).
+__device__ __forceinline__ void report_nonfinite(const KArgs& a, uint32_t bad) {
+  if (bad && a.nonfinite) atomicOr(a.nonfinite, 1);
+}
 
 // First run whose end is > idx.
 __device__ __forceinline__ int find_run_lds(int nruns, int64_t idx) {
@@ -347,7 +360,7 @@ struct StepTraits {
 // no branch inside, no bounds checks, every load issued before any arithmetic.
 template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL, bool PRIOR, bool GR>
 __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, int64_t gb,
-                                           float eta, float ns, float* gp) {
+                                           float eta, float ns, float* gp, uint32_t& bad) {
   using T = StepTraits<METHOD, COLLECT>;
   constexpr bool kPriorLoad = T::kReadPrior && PRIOR && !GR;
   f4v th[UNROLL], g[UNROLL], v[UNROLL], t0[UNROLL], ep[UNROLL], m1[UNROLL], m2[UNROLL];
@@ -386,8 +399,14 @@ __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, i
       m1[u][j] = x1;
       m2[u][j] = x2;
     }
-    if constexpr (T::kWriteTheta) vstore(a.theta + e, th[u]);
-    if constexpr (T::kWriteGrad) vstore(gp + e, g[u]);
+    if constexpr (T::kWriteTheta) {
+      bad |= nonfinite4(th[u]);
+      vstore(a.theta + e, th[u]);
+    }
+    if constexpr (T::kWriteGrad) {
+      bad |= nonfinite4(g[u]);
+      vstore(gp + e, g[u]);
+    }
     if constexpr (T::kMom) vstore(a.mom + e, v[u]);
     if constexpr (METHOD == BDL_SGLD) {
       if (c.sgd_mom) vstore(a.mom + e, v[u]);
@@ -401,23 +420,24 @@ __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, i
 
 template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
 __device__ __forceinline__ void chunk_fast_dispatch(const KArgs& a, const StepConst& c,
-                                                    int64_t gb, uint32_t attr, float* gp) {
+                                                    int64_t gb, uint32_t attr, float* gp,
+                                                    uint32_t& bad) {
   const bool head = (attr & BDL_ATTR_HEAD) != 0;
   const float eta = head ? a.lr1 : a.lr0;
   const float ns = head ? a.ns1 : a.ns0;
   if constexpr (METHOD == BDL_CSGHMC) {
-    chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(a, c, gb, eta, ns, gp);
+    chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(a, c, gb, eta, ns, gp, bad);
   } else {
     if constexpr (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) {
       if (c.grad_ready) {
-        chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, true>(a, c, gb, eta, ns, gp);
+        chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, true>(a, c, gb, eta, ns, gp, bad);
         return;
       }
     }
     if (attr & BDL_ATTR_PRIOR)
-      chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, true, false>(a, c, gb, eta, ns, gp);
+      chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, true, false>(a, c, gb, eta, ns, gp, bad);
     else
-      chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(a, c, gb, eta, ns, gp);
+      chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(a, c, gb, eta, ns, gp, bad);
   }
 }
 
@@ -448,7 +468,7 @@ __device__ __forceinline__ void update_elem(const KArgs& a, const StepConst& c, 
 // O(#runs + #blocks) iterations per launch.
 template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
 __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, int64_t gb,
-                                           int64_t gend, int r0) {
+                                           int64_t gend, int r0, uint32_t& bad) {
   using T = StepTraits<METHOD, COLLECT>;
   const int64_t n = a.n;
   int rr = r0;  // run of the chunk's first element; a lane's elements only move forward
@@ -485,7 +505,11 @@ __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, i
       m1[j] = x1;
       m2[j] = x2;
     }
-    if (T::kWriteTheta) st4(a.theta, e, n, th);
+    if (T::kWriteTheta) {
+      bad |= nonfinite4(th);  // lanes past n hold 0: never flagged
+      st4(a.theta, e, n, th);
+    }
+    if (T::kWriteGrad) bad |= nonfinite4(g);  // SKIP elements hold 0 here
     if (T::kWriteGrad && !gt) st4(a.grad, e, n, g);
     if (T::kMom || (METHOD == BDL_SGLD && c.sgd_mom)) st4(a.mom, e, n, v);
     if (T::kCollect) {
@@ -532,16 +556,19 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
   if (g0 >= g1) return;
 
   int r = find_run_lds(a.nruns, g0 * 4);
+  uint32_t bad = 0;
   for (int64_t gb = g0; gb < g1; gb += gstep) {
     while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
     const int64_t gend = min(gb + kIter, g1);
     const uint32_t attr = run_attr(r);
     if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 &&
         !(attr & kNoFastPath))
-      chunk_fast_dispatch<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, attr, run_grad(a, r));
+      chunk_fast_dispatch<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, attr, run_grad(a, r),
+                                                                  bad);
     else
-      chunk_slow<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, gend, r);
+      chunk_slow<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, gend, r, bad);
   }
+  report_nonfinite(a, bad);
 }
 
 template <int METHOD, int NOISE, int COLLECT, int UNROLL>
@@ -604,7 +631,7 @@ __device__ __forceinline__ void adam_core(const KArgs& a, const AdamConst& c, fl
 
 template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, bool PRIOR, int U>
 __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, int64_t gb,
-                                          float eta, float* gp) {
+                                          float eta, float* gp, uint32_t& bad) {
   constexpr bool kReadMoments = (COLLECT == BDL_COLLECT_MEAN);
   const f4v z = {0.f, 0.f, 0.f, 0.f};
   f4v th[U], g[U], vm[U], m[U], v[U], buf[U], t0[U], ep[U], m1[U], m2[U];
@@ -649,10 +676,13 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
       m1[u][j] = x1;
       m2[u][j] = x2;
     }
-    if constexpr (GRADONLY)
+    if constexpr (GRADONLY) {
+      bad |= nonfinite4(g[u]);
       vstore(gp + e, g[u]);
-    else
+    } else {
+      bad |= nonfinite4(th[u]);
       vstore(a.theta + e, th[u]);
+    }
     vstore(a.mom + e, vm[u]);
     vstore(a.adam_m + e, m[u]);
     vstore(a.adam_v + e, v[u]);
@@ -666,7 +696,7 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
 
 template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, int U>
 __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, int64_t gb,
-                                          int64_t gend, int r0) {
+                                          int64_t gend, int r0, uint32_t& bad) {
   const int64_t n = a.n;
   int rr = r0;  // run of the chunk's first element; a lane's elements only move forward
   const f4v z = {0.f, 0.f, 0.f, 0.f};
@@ -715,8 +745,10 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
       m2[j] = x2;
     }
     if (GRADONLY) {
+      bad |= nonfinite4(g);
       if (!gt) st4(a.grad, e, n, g);
     } else {
+      bad |= nonfinite4(th);
       st4(a.theta, e, n, th);
     }
     st4(a.mom, e, n, vm);
@@ -748,6 +780,7 @@ __device__ __forceinline__ void adam_body(const KArgs& a) {
   const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
   stage_runs(a);
   int r = find_run_lds(a.nruns, (int64_t)blockIdx.x * kIter * 4);
+  uint32_t bad = 0;
   for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {
     while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
     const int64_t gend = min(gb + kIter, ngroups);
@@ -755,13 +788,14 @@ __device__ __forceinline__ void adam_body(const KArgs& a) {
     if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 && !(attr & kNoFastPath)) {
       const float eta = (attr & BDL_ATTR_HEAD) ? a.lr1 : a.lr0;
       if (attr & BDL_ATTR_PRIOR)
-        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, true, U>(a, c, gb, eta, run_grad(a, r));
+        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, true, U>(a, c, gb, eta, run_grad(a, r), bad);
       else
-        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, false, U>(a, c, gb, eta, run_grad(a, r));
+        adam_fast<NOISE, COLLECT, RECIP, GRADONLY, false, U>(a, c, gb, eta, run_grad(a, r), bad);
     } else {
-      adam_slow<NOISE, COLLECT, RECIP, GRADONLY, U>(a, c, gb, gend, r);
+      adam_slow<NOISE, COLLECT, RECIP, GRADONLY, U>(a, c, gb, gend, r, bad);
     }
   }
+  report_nonfinite(a, bad);
 }
 
 template <int NOISE, int COLLECT, bool GRADONLY, int U>

@@ -217,6 +217,8 @@ class FlatState:
                     for q, o, k in zip(p0, self.offsets, self.numels):
                         self.prior[o:o + k].copy_(q.detach().reshape(-1))
         self.noise = torch.empty(self.n, dtype=torch.float32, device=dev) if need_noise else None
+        # divergence flag the step kernels set on a non-finite theta / grad
+        self.nonfinite = torch.zeros(1, dtype=torch.int32, device=dev)
 
         attrs = segment_attrs(self.names, self.readout_name, bias, self.requires_grad)
         self.attrs = attrs
@@ -278,6 +280,7 @@ class FlatState:
         self.mom = vecs["mom"].zero_() if need_mom else None
         self.prior = vecs["prior"].zero_() if need_prior else None
         self.noise = torch.empty(self.n, **f32) if need_noise else None
+        self.nonfinite = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.attrs = segment_attrs(self.names, readout_name, bias, self.requires_grad)
         self.runs = build_runs(self.offsets, self.numels, self.attrs, self.n).to(self.device)
         self.nruns = int(self.runs.shape[0])
@@ -427,6 +430,14 @@ class FlatState:
             h[2 * nt + i] = base
         dev = host.to(self.device, non_blocking=True)
         return dev[:2 * nt].view(nt, 2), nt, dev[2 * nt:]
+
+    def diverged(self, reset=True):
+        """Did any step since the last reset write a non-finite theta / grad?
+        (One device-to-host read: call it at epoch granularity, not per step.)"""
+        bad = bool(self.nonfinite.item())
+        if bad and reset:
+            self.nonfinite.zero_()
+        return bad
 
     def grad_table(self):
         """The run / gradient-base selection of the current step (to reuse

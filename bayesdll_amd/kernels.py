@@ -45,6 +45,8 @@ def _step_args(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1
     a.grad = None if g is None else g.data_ptr()
     gb = getattr(state, "gbase", None)  # per-tensor gradients ("tensor" grad mode)
     a.grad_base = None if gb is None else gb.data_ptr()
+    nf = getattr(state, "nonfinite", None)  # divergence flag (FlatState.nonfinite)
+    a.nonfinite = None if nf is None else nf.data_ptr()
     mb = state.mom if mom_buf is None else mom_buf  # mom_buf: a separate SGD buffer
     a.mom = None if mb is None else mb.data_ptr()
     a.prior_mean = None if state.prior is None else state.prior.data_ptr()

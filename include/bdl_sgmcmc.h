@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define BDL_ABI_VERSION 3
+#define BDL_ABI_VERSION 4
 
 typedef enum bdl_status {
   BDL_OK = 0,
@@ -179,6 +179,11 @@ typedef struct bdl_step_args {
    * SKIP runs may hold 0; a base that is not 16-byte aligned needs
    * BDL_ATTR_GUNALIGNED on its run.  `grad` may be null in this mode. */
   const int64_t* grad_base;
+  /* Divergence guard (nullable): set to 1 (atomic OR) when the step writes a
+   * theta value (or, for *_GRAD methods, a gradient value) that is NaN or
+   * +-Inf.  Never written on a healthy chain; the host reads it when it likes
+   * (e.g. once per epoch), so the guard adds no synchronisation. */
+  int32_t* nonfinite;
 } bdl_step_args;
 
 /* Extra state and scalars of the Adam-preconditioned SGHMC step.  Per element,

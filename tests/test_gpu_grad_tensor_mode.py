@@ -244,3 +244,78 @@ def test_frozen_parameters_tensor_vs_flat(method):
             os.environ.pop("BDL_GRAD_MODE", None)
 
     assert torch.equal(run("tensor"), run("flat"))
+
+
+@pytest.mark.parametrize("where", ["fast", "tail"])
+@pytest.mark.parametrize("method", ["csghmc", "sgld", "sgld_grad", "adam"])
+def test_divergence_flag(method, where):
+    """bdl_step_args.nonfinite: a step that writes a NaN / Inf theta (or
+    gradient, *_GRAD) raises the device flag — from the unrolled fast path and
+    from the guarded tail; a healthy step leaves it 0."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.flat import FlatState
+    segs = [("w", (70001,)), ("classifier.weight", (10, 30))]  # n = 70301: a ragged tail
+    st = FlatState.from_segments(segs, "classifier", device=DEV, need_prior=True,
+                                 extra=("adam_m", "adam_v") if method == "adam" else ())
+    g = torch.Generator(device=DEV).manual_seed(3)
+    st.theta.normal_(0, 0.02, generator=g)
+    st.grad.normal_(0, 1e-3, generator=g)
+
+    def step():
+        kw = dict(lrs=(1e-3, 1e-3), noise_mode=L.NOISE_PHILOX, seed=1, step=0)
+        if method == "csghmc":
+            K.sgmcmc_step(st, L.CSGHMC, noise_scale=(1e-3, 1e-3), one_minus_alpha=0.9,
+                          prior_sig=1.0, **kw)
+        elif method in ("sgld", "sgld_grad"):
+            K.sgmcmc_step(st, L.SGLD if method == "sgld" else L.SGLD_GRAD,
+                          noise_scale=(1e-3, 1e-3), sigma2=1.0, n_data=1e3, **kw)
+        else:
+            K.adam_step(st, L.ADAM_SGHMC, adam_m=st.extra["adam_m"], adam_v=st.extra["adam_v"],
+                        beta1=0.9, beta2=0.999, eps=1e-8, t=1, momentum_decay=0.1, nd=0.01,
+                        sigma2=1.0, n_data=1e3, **kw)
+        torch.cuda.synchronize()
+
+    step()
+    assert not st.diverged()
+    idx = 1000 if where == "fast" else st.n - 2
+    st.grad[idx] = float("nan") if method != "adam" else float("inf")
+    step()
+    assert st.diverged()          # reads and resets
+    assert not st.diverged()
+    st.grad.normal_(0, 1e-3, generator=g)
+    st.theta.normal_(0, 0.02, generator=g)
+    if method == "adam":
+        st.extra["adam_m"].zero_()
+        st.extra["adam_v"].zero_()
+    st.mom.zero_()
+    step()
+    assert not st.diverged()
+
+
+def test_runner_reports_divergence():
+    """A cSGHMC chain with an absurd step size blows up; the Runner notices at
+    the epoch boundary (one flag read per epoch) and records the epoch."""
+    import logging
+    import tempfile
+    from types import SimpleNamespace
+    import bayesdll_amd.csghmc as csghmc
+    from fakenet import MLP, synthetic_mnist
+    train = synthetic_mnist(61, 128, 64, device=DEV)
+    test = synthetic_mnist(62, 64, 64, device=DEV)
+
+    def run(lr):
+        torch.manual_seed(0)
+        args = SimpleNamespace(device=DEV, ND=128, pretrained=None, lr=lr, lr_head=lr,
+                               momentum=0.0, epochs=2, num_cycles=1, proportion_exploration=0.5,
+                               full_sample=False, test_eval_freq=100, ece_num_bins=15,
+                               log_dir=tempfile.mkdtemp(), num_classes=10,
+                               hparams={"prior_sig": "1.0", "bias": "informative",
+                                        "momentum_decay": "0.1", "Ninflate": "1.0",
+                                        "nd": "0.0", "burnin": "0", "thin": "100", "nst": "0"})
+        r = csghmc.Runner(MLP().to(DEV), None, args, logging.getLogger("div"))
+        r.train(train, None, test)
+        return r.diverged_epochs
+
+    assert run(1e-3) == []
+    assert run(1e38) != []
