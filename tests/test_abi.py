@@ -258,3 +258,127 @@ def test_reference_written_checkpoints_load_weights_only():
                        "prior_sig", "optimizer", "epoch"}
     n = sum(v.numel() for v in ck["last_theta"].values())
     assert ck["post_theta_mom1"].numel() == n and isinstance(ck["post_theta_mom1"], torch.Tensor)
+
+
+ASAN_HOST = r"""
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "bdl_sgmcmc.h"
+static unsigned long long s = 88172645463325252ULL;
+static unsigned long long rnd(void) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; }
+#define EXPECT(c) do { if (!(c)) { printf("FAIL line %d\n", __LINE__); return 1; } } while (0)
+int main(void) {
+  long ok = 0, rejected = 0;
+  for (int it = 0; it < 4000; ++it) {           /* bdl_build_runs on random tables */
+    int nseg = (int)(rnd() % 40);
+    bdl_segment* segs = (bdl_segment*)malloc(sizeof(bdl_segment) * (nseg ? nseg : 1));
+    long long pos = 0;
+    for (int i = 0; i < nseg; ++i) {
+      long long gap = (rnd() % 4 == 0) ? (long long)(rnd() % 5) : 0;
+      if (rnd() % 97 == 0) gap = -(long long)(1 + rnd() % 3);   /* overlap */
+      long long k = (long long)(rnd() % 50);
+      segs[i].offset = pos + gap; segs[i].numel = k;
+      segs[i].attr = (unsigned)(rnd() % 16); segs[i].pad = 0;
+      pos = segs[i].offset + k;
+    }
+    long long n = pos + (long long)(rnd() % 5);
+    if (rnd() % 50 == 0) n = pos - 1;                             /* segment past n */
+    int cap = (rnd() % 3 == 0) ? (int)(rnd() % (2 * nseg + 3)) : 2 * nseg + 2;
+    if (cap < 1) cap = 1;
+    bdl_run* runs = (bdl_run*)malloc(sizeof(bdl_run) * cap);
+    int nr = bdl_build_runs(segs, nseg, n, runs, cap);
+    if (nr > 0) {
+      EXPECT(nr <= cap);
+      for (int r = 1; r < nr; ++r) EXPECT(runs[r].end > runs[r - 1].end && runs[r].attr != runs[r - 1].attr);
+      EXPECT(runs[nr - 1].end == n);
+      int r = 0;
+      for (long long e = 0; e < n; ++e) {                          /* every element's attributes */
+        unsigned want = BDL_ATTR_SKIP;
+        for (int i = 0; i < nseg; ++i)
+          if (e >= segs[i].offset && e < segs[i].offset + segs[i].numel) want = segs[i].attr & 0xF;
+        while (runs[r].end <= e) ++r;
+        EXPECT(runs[r].attr == want);
+      }
+      ++ok;
+    } else {
+      EXPECT(nr < 0 && strlen(bdl_last_error()) > 0);
+      ++rejected;
+    }
+    free(segs);
+    free(runs);
+  }
+  /* argument validation of every entry point (returns before any device call) */
+  bdl_step_args a; memset(&a, 0, sizeof a);
+  a.n = 16; a.method = BDL_CSGHMC;
+  EXPECT(bdl_sgmcmc_step(NULL, NULL) == BDL_ERR_NULL);
+  EXPECT(bdl_sgmcmc_step(&a, NULL) == BDL_ERR_NULL);
+  a.theta = (float*)0x1000; a.runs = (const bdl_run*)0x4000; a.nruns = 1; a.mom = (float*)0x3000;
+  EXPECT(bdl_sgmcmc_step(&a, NULL) == BDL_ERR_NULL);            /* no grad, no grad_base */
+  a.grad_base = (const int64_t*)0x5004;
+  EXPECT(bdl_sgmcmc_step(&a, NULL) == BDL_ERR_ALIGN);
+  a.grad_base = (const int64_t*)0x5000; a.nruns = 2731;
+  EXPECT(bdl_sgmcmc_step(&a, NULL) == BDL_ERR_RUNS);
+  a.grad_base = NULL; a.grad = (float*)0x2000; a.nruns = 4097;
+  EXPECT(bdl_sgmcmc_step(&a, NULL) == BDL_ERR_RUNS);
+  a.nruns = 1; a.theta = (float*)0x1004;
+  EXPECT(bdl_sgmcmc_step(&a, NULL) == BDL_ERR_ALIGN);
+  a.theta = (float*)0x1000; a.method = 99;
+  EXPECT(bdl_sgmcmc_step(&a, NULL) == BDL_ERR_ARG);
+  a.method = BDL_SGLD;
+  EXPECT(bdl_sgmcmc_step(&a, NULL) == BDL_ERR_NULL);            /* prior_mean */
+  a.method = BDL_SGLD_GRAD; a.prior_mean = (const float*)0x6000; a.collect = BDL_COLLECT_MEAN;
+  a.mom1 = (float*)0x7000;
+  EXPECT(bdl_sgmcmc_step(&a, NULL) == BDL_ERR_ARG);             /* grad-only cannot collect */
+  EXPECT(bdl_sgld_step_clipped(&a, 1.0f, (void*)0x8000, NULL) == BDL_ERR_ARG);
+  a.method = BDL_SGLD; a.collect = 0;
+  EXPECT(bdl_sgld_step_clipped(&a, 0.0f, (void*)0x8000, NULL) == BDL_ERR_ARG);
+  EXPECT(bdl_sgld_step_clipped(&a, 1.0f, (void*)0x8004, NULL) == BDL_ERR_ALIGN);
+  bdl_adam_args ad; memset(&ad, 0, sizeof ad);
+  a.method = BDL_ADAM_SGHMC;
+  EXPECT(bdl_adam_step(&a, &ad, NULL) == BDL_ERR_NULL);         /* adam_m / adam_v */
+  EXPECT(bdl_adam_step(&a, NULL, NULL) == BDL_ERR_NULL);
+  bdl_moments_args m; memset(&m, 0, sizeof m); m.n = 8; m.collect = 9;
+  EXPECT(bdl_moments_update(&m, NULL) == BDL_ERR_ARG);
+  m.collect = BDL_COLLECT_MEAN;
+  EXPECT(bdl_moments_update(&m, NULL) == BDL_ERR_NULL);
+  bdl_sample_args sa; memset(&sa, 0, sizeof sa); sa.n = 8; sa.var_mode = 7;
+  EXPECT(bdl_posterior_sample(&sa, NULL) == BDL_ERR_ARG);
+  EXPECT(bdl_philox_normal(NULL, 8, 0, 0, 0, NULL) == BDL_ERR_NULL);
+  EXPECT(bdl_philox_normal((float*)0x1004, 8, 0, 0, 0, NULL) == BDL_ERR_ALIGN);
+  printf("OK %ld %ld\n", ok, rejected);
+  return 0;
+}
+"""
+
+
+def test_host_abi_under_address_sanitizer(tmp_path):
+    """SURVEY §5 'race detection / sanitizers': the C-ABI's host code (run
+    building, every entry point's validation and error paths) built with
+    host-side AddressSanitizer (`make asan`; device code unchanged, GPU
+    sanitizers are not available) and driven by a C host over 4000 random
+    segment tables (gaps, overlaps, segments past n, undersized outputs) —
+    no ASan report, every accepted table exactly right, every rejected one
+    with a message.  No device calls."""
+    import shutil
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    csrc = os.path.join(root, "bayesdll_amd", "csrc")
+    lib = os.path.join(root, "bayesdll_amd", "libbdl_sgmcmc_asan.so")
+    subprocess.check_call(["make", "-C", csrc, "-j8", "asan"], stdout=subprocess.DEVNULL)
+    clang = "/opt/rocm/lib/llvm/bin/clang"
+    if not os.path.exists(clang):
+        clang = shutil.which("clang")
+    c = tmp_path / "fuzz.c"
+    exe = tmp_path / "fuzz"
+    c.write_text(ASAN_HOST)
+    shutil.copy(lib, tmp_path / "libbdl_sgmcmc_asan.so")
+    subprocess.check_call([clang, "-std=c99", "-g", "-fsanitize=address", "-fno-omit-frame-pointer",
+                           "-I", os.path.dirname(HEADER), str(c), "-o", str(exe),
+                           "-L", str(tmp_path), "-lbdl_sgmcmc_asan", f"-Wl,-rpath,{tmp_path}",
+                           "-Wl,-rpath,/opt/rocm/lib"])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0:abort_on_error=0")
+    p = subprocess.run([str(exe)], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and p.stdout.startswith("OK"), (p.stdout + p.stderr)[-3000:]
+    assert "AddressSanitizer" not in p.stderr
+    ok, rejected = map(int, p.stdout.split()[1:3])
+    assert ok > 1000 and rejected > 10
