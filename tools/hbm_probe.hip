@@ -29,13 +29,24 @@ __device__ __forceinline__ void st(f4* p, f4 v) {
     *p = v;
 }
 
-template <int MODE, bool NT, int U>
+// XCD remap (XCD=1): workgroups are dispatched round-robin over the 8 XCDs
+// (block b runs on XCD b % 8); remapped, XCD x sweeps the logical blocks
+// [x*G/8, (x+1)*G/8) of every grid-stride window, i.e. one contiguous 1/8 of it.
+template <bool XCD>
+__device__ __forceinline__ long logical_block() {
+  if constexpr (!XCD) return blockIdx.x;
+  const long g = gridDim.x, per = g / 8;
+  const long b = blockIdx.x;
+  return (g % 8 == 0) ? (b % 8) * per + b / 8 : b;
+}
+
+template <int MODE, bool NT, int U, bool XCD = false>
 __global__ __launch_bounds__(256) void probe(const f4* __restrict__ a, const f4* __restrict__ b,
                                              const f4* __restrict__ c, f4* __restrict__ x,
                                              f4* __restrict__ y, long n4, float* sink) {
   const long step = (long)gridDim.x * 256 * U;
   f4 acc = {0, 0, 0, 0};
-  for (long base = (long)blockIdx.x * 256 * U; base < n4; base += step) {
+  for (long base = logical_block<XCD>() * 256 * U; base < n4; base += step) {
     f4 ra[U], rb[U], rc[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -75,15 +86,15 @@ __global__ __launch_bounds__(256) void probe(const f4* __restrict__ a, const f4*
     }                                                                            \
   } while (0)
 
-template <int MODE, bool NT, int U>
+template <int MODE, bool NT, int U, bool XCD = false>
 float run(int grid, const f4* a, const f4* b, const f4* c, f4* x, f4* y, long n4, float* sink,
           int reps) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  for (int i = 0; i < 3; ++i) probe<MODE, NT, U><<<grid, 256>>>(a, b, c, x, y, n4, sink);
+  for (int i = 0; i < 3; ++i) probe<MODE, NT, U, XCD><<<grid, 256>>>(a, b, c, x, y, n4, sink);
   CHECK(hipEventRecord(e0));
-  for (int i = 0; i < reps; ++i) probe<MODE, NT, U><<<grid, 256>>>(a, b, c, x, y, n4, sink);
+  for (int i = 0; i < reps; ++i) probe<MODE, NT, U, XCD><<<grid, 256>>>(a, b, c, x, y, n4, sink);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   float ms = 0;
@@ -93,16 +104,16 @@ float run(int grid, const f4* a, const f4* b, const f4* c, f4* x, f4* y, long n4
   return ms / reps;
 }
 
-template <int MODE, bool NT, int U>
+template <int MODE, bool NT, int U, bool XCD = false>
 void sweep(const char* name, int cus, const f4* a, const f4* b, const f4* c, f4* x, f4* y, long n4,
            float* sink) {
   const double bytes_per_el = (MODE == 0 || MODE == 1) ? 4 : (MODE == 2 ? 8 : 20);
   const int bpcs[] = {1, 2, 3, 4};
   for (int bpc : bpcs) {
-    const float ms = run<MODE, NT, U>(cus * bpc, a, b, c, x, y, n4, sink, 20);
-    printf("{\"pattern\": \"%s\", \"nt\": %d, \"unroll\": %d, \"blocks_per_cu\": %d, \"ms\": %.4f, "
-           "\"gbs\": %.1f}\n",
-           name, NT ? 1 : 0, U, bpc, ms, bytes_per_el * n4 * 4 / ms / 1e6);
+    const float ms = run<MODE, NT, U, XCD>(cus * bpc, a, b, c, x, y, n4, sink, 20);
+    printf("{\"pattern\": \"%s\", \"nt\": %d, \"unroll\": %d, \"blocks_per_cu\": %d, "
+           "\"xcd_remap\": %d, \"ms\": %.4f, \"gbs\": %.1f}\n",
+           name, NT ? 1 : 0, U, bpc, XCD ? 1 : 0, ms, bytes_per_el * n4 * 4 / ms / 1e6);
     fflush(stdout);
   }
 }
@@ -126,6 +137,16 @@ int main() {
   CHECK(hipMemset(c, 0, n4 * sizeof(f4)));
   const char* which = getenv("PROBE") ? getenv("PROBE") : "all";
   const bool all = !strcmp(which, "all");
+  if (!strcmp(which, "xcd")) {  // XCD-remapped vs round-robin block order, the explore mix
+    for (int rep = 0; rep < 2; ++rep) {
+      sweep<4, true, 4, false>("r3w2_inplace", cus, a, b, c, x, y, n4, sink);
+      sweep<4, true, 4, true>("r3w2_inplace", cus, a, b, c, x, y, n4, sink);
+      sweep<4, true, 2, false>("r3w2_inplace", cus, a, b, c, x, y, n4, sink);
+      sweep<4, true, 2, true>("r3w2_inplace", cus, a, b, c, x, y, n4, sink);
+    }
+    CHECK(hipDeviceSynchronize());
+    return 0;
+  }
   if (all) {
     sweep<0, false, 2>("read1", cus, a, b, c, x, y, n4, sink);
     sweep<0, true, 2>("read1", cus, a, b, c, x, y, n4, sink);
