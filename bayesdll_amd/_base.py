@@ -82,6 +82,10 @@ class FusedModelBase(nn.Module):
                                     need_noise=self.noise_mode != "philox",
                                     placement=self.tune_method, extra=self.extra_vectors)
             self._state_net = net
+            steps_timed = int(os.environ.get("BDL_STEP_TIMING", "0") or 0)
+            if steps_timed > 0:  # sampled update timing, logged once per epoch
+                from . import kernels as K
+                self._state.timer = K.StepTimer(steps_timed)
             # launch geometry for this device and size (speed only: results
             # never depend on it)
             from . import kernels as K

@@ -80,6 +80,22 @@ def check_divergence(runner, ep):
                               "diverged (step size too large for the gradient scale?)")
 
 
+def log_update_stats(runner, ep):
+    """BDL_STEP_TIMING=k: one log line per epoch with the fused update's
+    launch count, sampled mean duration and algorithmic HBM GB/s."""
+    st = runner.model.flat
+    t = getattr(st, "timer", None) if st is not None else None
+    if t is None:
+        return None
+    s = t.summary()
+    if s.get("timed"):
+        runner.logger.info(f"[Epoch {ep}] fused update: {s['launches']} launches, "
+                           f"{s['avg_ms']:.4f} ms mean over {s['timed']} sampled, "
+                           f"{s['gbs']:.1f} GB/s algorithmic ({100 * s['gbs'] / 8000.0:.1f} % of "
+                           "8 TB/s HBM3E)")
+    return s
+
+
 def bind_chain_log_dir(args):
     """With several chains (one per rank) sharing a log_dir, every chain writes
     its checkpoints / logits / snapshots under <log_dir>/chain<rank> (the

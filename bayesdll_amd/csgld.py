@@ -112,6 +112,7 @@ class Runner:
             tic = time.time()
             losses_train[ep], errors_train[ep], cycle_updated = self.train_one_epoch(train_loader)
             R.check_divergence(self, ep)
+            R.log_update_stats(self, ep)
             logger.info(f"[Epoch {ep}/{args.epochs}] Training summary: loss = "
                         f"{losses_train[ep]:.4f}, prediction error = {errors_train[ep]:.4f} "
                         f"(time: {time.time() - tic:.4f} seconds)")

@@ -79,10 +79,81 @@ def _step_args(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1
     return a
 
 
+def alg_bytes_per_elem(a, adam=None):
+    """Algorithmic HBM bytes per element of one step launch: 4 B
+    per vector read, 4 B per vector written, from the launch's own arguments."""
+    grad_only = a.method in (L.SGHMC_GRAD, L.SGLD_GRAD, L.ADAM_SGHMC_GRAD)
+    b = 4 + (0 if grad_only else 4)                      # theta r (+w)
+    b += 4 + (4 if grad_only else 0)                     # grad r (+w)
+    if a.method in (L.CSGHMC, L.SGHMC, L.SGHMC_GRAD, L.ADAM_SGHMC, L.ADAM_SGHMC_GRAD):
+        b += 8                                           # momentum v r+w
+    elif a.method == L.SGLD and a.flags & L.FLAG_MOMENTUM:
+        b += 4 if a.flags & L.FLAG_FIRST_STEP else 8     # SGD buffer (w | r+w)
+    if a.method != L.CSGHMC and a.prior_mean:
+        b += 4                                           # theta0 r
+    if a.noise_mode == L.NOISE_BUFFER:
+        b += 4
+    if adam is not None:
+        b += 16                                          # Adam m, v r+w
+        if adam.sgd_buf:
+            b += 4 if a.flags & L.FLAG_FIRST_STEP else 8
+    nmom = 2 if a.mom2 else 1
+    if a.collect in (L.COLLECT_WELFORD, L.COLLECT_MEAN):
+        b += 8 * nmom
+    elif a.collect in (L.COLLECT_WELFORD_INIT, L.COLLECT_MEAN_INIT):
+        b += 4 * nmom
+    return b
+
+
+class StepTimer:
+    """Sampled HIP-event timing of the fused update launches (BDL_STEP_TIMING=k:
+    every k-th launch), on the launch stream; summary() once per epoch gives
+    launches, mean ms and algorithmic GB/s (expose step counters
+    and GB/s).  Off by default; never synchronises per step."""
+
+    def __init__(self, every):
+        self.every, self.count, self.recs = max(1, int(every)), 0, []
+
+    def begin(self):
+        self.count += 1
+        if (self.count - 1) % self.every:
+            return None
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return e0
+
+    def end(self, e0, nbytes):
+        if e0 is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.recs.append((e0, e1, nbytes))
+
+    def summary(self, reset=True):
+        if not self.recs:
+            return {"launches": self.count, "timed": 0}
+        self.recs[-1][1].synchronize()
+        ms = [a.elapsed_time(b) for a, b, _ in self.recs]
+        gbs = [nb / (t * 1e-3) / 1e9 for t, (_, _, nb) in zip(ms, self.recs)]
+        out = {"launches": self.count, "timed": len(ms), "avg_ms": sum(ms) / len(ms),
+               "gbs": sum(gbs) / len(gbs)}
+        if reset:
+            self.count, self.recs = 0, []
+        return out
+
+
+def _launch(state, fn, a, adam=None):
+    t = getattr(state, "timer", None)
+    e0 = t.begin() if t is not None else None
+    fn()
+    if e0 is not None:
+        t.end(e0, alg_bytes_per_elem(a, adam) * int(a.n))
+
+
 def sgmcmc_step(state, method, **kw):
     """One fused update over `state` (a FlatState). Asynchronous."""
     a = _step_args(state, method, **kw)
-    L.check(L.lib().bdl_sgmcmc_step(a, L.current_stream_handle(state.device)), "bdl_sgmcmc_step")
+    _launch(state, lambda: L.check(L.lib().bdl_sgmcmc_step(a, L.current_stream_handle(state.device)),
+                                   "bdl_sgmcmc_step"), a)
 
 
 def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps, t,
@@ -114,7 +185,8 @@ def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps,
     ad.inv_bias_corr1, ad.inv_bias_corr2 = _inv(bc1), _inv(bc2)
     ad.inv_temperature = _inv(temperature)
     ad.grad_is_mom = 1 if grad_is_mom else 0
-    L.check(L.lib().bdl_adam_step(a, ad, L.current_stream_handle(state.device)), "bdl_adam_step")
+    _launch(state, lambda: L.check(L.lib().bdl_adam_step(a, ad, L.current_stream_handle(state.device)),
+                                   "bdl_adam_step"), a, ad)
 
 
 def clip_workspace(state):

@@ -382,3 +382,31 @@ def test_host_abi_under_address_sanitizer(tmp_path):
     assert "AddressSanitizer" not in p.stderr
     ok, rejected = map(int, p.stdout.split()[1:3])
     assert ok > 1000 and rejected > 10
+
+
+def test_algorithmic_bytes_per_element_match_design_table():
+    """kernels.alg_bytes_per_elem (used by the per-epoch GB/s log) reproduces
+    DESIGN §4's table / bench.BYTES_PER_ELEM from a launch's own arguments."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd.kernels import alg_bytes_per_elem
+
+    def args(method, collect=0, flags=0, prior=True, m2=True, noise=L.NOISE_PHILOX):
+        a = L.StepArgs()
+        a.method, a.collect, a.flags, a.noise_mode = method, collect, flags, noise
+        a.prior_mean = 0x1000 if prior else None
+        a.mom2 = 0x2000 if m2 else None
+        return a
+    assert alg_bytes_per_elem(args(L.CSGHMC, prior=False, noise=L.NOISE_NONE)) == 20
+    assert alg_bytes_per_elem(args(L.CSGHMC, L.COLLECT_WELFORD_INIT, prior=False)) == 28
+    assert alg_bytes_per_elem(args(L.CSGHMC, L.COLLECT_WELFORD, prior=False)) == 36
+    assert alg_bytes_per_elem(args(L.CSGHMC, prior=False, noise=L.NOISE_BUFFER)) == 24
+    mom = L.FLAG_MOMENTUM
+    assert alg_bytes_per_elem(args(L.SGLD, flags=mom)) == 24
+    assert alg_bytes_per_elem(args(L.SGLD, flags=mom | L.FLAG_FIRST_STEP)) == 20
+    assert alg_bytes_per_elem(args(L.SGLD, L.COLLECT_MEAN, flags=mom)) == 40
+    assert alg_bytes_per_elem(args(L.SGHMC)) == 24
+    ad = L.AdamArgs()
+    ad.sgd_buf = 0x3000
+    assert alg_bytes_per_elem(args(L.ADAM_SGHMC, flags=mom), ad) == 48
+    assert alg_bytes_per_elem(args(L.ADAM_SGHMC, flags=mom | L.FLAG_FIRST_STEP), ad) == 44
+    assert alg_bytes_per_elem(args(L.ADAM_SGHMC, L.COLLECT_MEAN, flags=mom), ad) == 64

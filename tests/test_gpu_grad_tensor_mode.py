@@ -319,3 +319,33 @@ def test_runner_reports_divergence():
 
     assert run(1e-3) == []
     assert run(1e38) != []
+
+
+def test_step_timing_log(caplog):
+    """BDL_STEP_TIMING=k: sampled HIP-event timing of the fused update and one
+    log line per epoch with launches, mean ms and algorithmic GB/s."""
+    import logging
+    import os
+    import tempfile
+    from types import SimpleNamespace
+    import bayesdll_amd.csghmc as csghmc
+    from fakenet import MLP, synthetic_mnist
+    train = synthetic_mnist(71, 256, 64, device=DEV)
+    os.environ["BDL_STEP_TIMING"] = "2"
+    try:
+        args = SimpleNamespace(device=DEV, ND=256, pretrained=None, lr=1e-3, lr_head=1e-3,
+                               momentum=0.0, epochs=2, num_cycles=2, proportion_exploration=0.5,
+                               full_sample=False, test_eval_freq=100, ece_num_bins=15,
+                               log_dir=tempfile.mkdtemp(), num_classes=10,
+                               hparams={"prior_sig": "1.0", "bias": "informative",
+                                        "momentum_decay": "0.1", "Ninflate": "1.0",
+                                        "nd": "0.01", "burnin": "0", "thin": "2", "nst": "0"})
+        torch.manual_seed(0)
+        log = logging.getLogger("timing")
+        with caplog.at_level(logging.INFO, logger="timing"):
+            r = csghmc.Runner(MLP().to(DEV), None, args, log)
+            r.train(train, None, synthetic_mnist(72, 64, 64, device=DEV))
+    finally:
+        os.environ.pop("BDL_STEP_TIMING", None)
+    lines = [m for m in caplog.messages if "fused update:" in m]
+    assert len(lines) == 2 and "4 launches" in lines[0] and "GB/s algorithmic" in lines[0]
