@@ -142,6 +142,7 @@ def placed_vectors(n, device, names, method, candidates=None):
 
 
 GRAD_MODES = ("tensor", "flat")
+MAX_TENSOR_RUNS = 2730  # 24 B per run in 64 KiB of LDS (bdl_step_args.grad_base)
 GRAD_TABLE_CACHE = 8  # device run/base tables kept per state (one per pointer set)
 
 
@@ -182,6 +183,12 @@ class FlatState:
         self.grad_mode = grad_mode or default_grad_mode()
         if self.grad_mode not in GRAD_MODES:
             raise ValueError(f"grad_mode must be one of {GRAD_MODES}")
+        if self.grad_mode == "tensor" and len(self.params) > MAX_TENSOR_RUNS:
+            # one run per tensor would not fit the kernels' LDS run table
+            import warnings
+            warnings.warn(f"bayesdll_amd: {len(self.params)} parameter tensors > "
+                          f"{MAX_TENSOR_RUNS}: using the flat gradient vector")
+            self.grad_mode = "flat"
 
         # the swept vectors, placed (see placed_vectors) when `placement` names
         # the sampler's kernel family (in "tensor" mode the timing uses a
