@@ -598,3 +598,51 @@ def test_runner_graph_mode_matches_eager(method, tmp_path):
     if res_e is not None:
         np.testing.assert_array_equal(res_g["losses_train"], res_e["losses_train"])
         np.testing.assert_array_equal(res_g["losses_test"], res_e["losses_test"])
+
+
+def test_graph_mode_with_batchnorm_matches_eager():
+    """Graph mode on a network with BatchNorm (train mode): the running
+    statistics are updated inside the replayed graph exactly as in eager
+    mode (the capture's warm-up passes leave them untouched), so parameters
+    AND buffers equal the eager run bit for bit."""
+    import bayesdll_amd.csghmc as csghmc
+    dev = "cuda"
+
+    class SmallCNN(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.conv = torch.nn.Conv2d(1, 8, 3, padding=1)
+            self.bn = torch.nn.BatchNorm2d(8)
+            self.fc = torch.nn.Linear(8 * 28 * 28, 10)
+            self.readout_name = "fc"
+
+        def forward(self, x):
+            return self.fc(torch.relu(self.bn(self.conv(x))).flatten(1))
+
+    data = synthetic_mnist(81, 192, 64, device=dev)
+    crit = torch.nn.CrossEntropyLoss()
+
+    def run(graph):
+        torch.manual_seed(0)
+        net = SmallCNN().to(dev)
+        model = csghmc.Model(1000.0, prior_sig=1.0, momentum_decay=0.1)
+        model.noise_mode, model.seed, model.graph = "philox", 4, graph
+        for ep in range(3):
+            for k, (x, y) in enumerate(data):
+                model(x, y, net, None, crit, [1e-3, 1e-3], 1.0, 0.1, should_sample=k == 1)
+        torch.cuda.synchronize()
+        return model, {k: v.detach().clone() for k, v in net.state_dict().items()}
+
+    # MIOpen's default convolution algorithms are not run-to-run deterministic
+    # (two eager runs already differ); the reference demos set deterministic
+    # mode (demo_mnist.py:74), under which eager and graph agree bit for bit
+    prev = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        m_g, sd_g = run(True)
+        m_e, sd_e = run(False)
+    finally:
+        torch.backends.cudnn.deterministic = prev
+    assert m_g._graphs and not m_e._graphs
+    for k in sd_e:
+        assert torch.equal(sd_g[k], sd_e[k]), k
