@@ -80,6 +80,17 @@ def check_divergence(runner, ep):
                               "diverged (step size too large for the gradient scale?)")
 
 
+def log_calibration(runner, targets_test, logits_test, targets_val=None, logits_val=None):
+    """After a new best evaluation, as the reference Runners do
+    (methods/csghmc.py:170-196, methods/sgld.py:160-186): ECE / MCE / NLL at
+    T = 1 and at the temperature fitted on the validation set, with the
+    reliability plots.  args.calibration = False skips it."""
+    if not getattr(runner.args, "calibration", True):
+        return None
+    from .calibration import log_calibration as _log
+    return _log(runner.args, runner.logger, targets_test, logits_test, targets_val, logits_val)
+
+
 def log_update_stats(runner, ep):
     """BDL_STEP_TIMING=k: one log line per epoch with the fused update's
     launch count, sampled mean duration and algorithmic HBM GB/s."""

@@ -128,6 +128,8 @@ class Runner:
                     if val_loader is not None:
                         R.save_logits(args, tv, lv, lav, suffix="val")
                     R.save_logits(args, tt, lt, lat, suffix="test")
+                    R.log_calibration(self, tt, lt, *((tv, lv) if val_loader is not None
+                                                      else (None, None)))
         toc0 = time.time()
         logger.info(f"Training done! Total time = {toc0 - tic0:.4f} "
                     f"(average per epoch = {(toc0 - tic0) / args.epochs:.4f}) seconds")

@@ -524,12 +524,45 @@ def run_ckpt_interop(methods, method, cfg):
                 eval_draws=np.int64(draws))
 
 
+def calibration_fixture():
+    """Reference calibration.analyze / find_optimal_temperature on seeded
+    logits (the metrics the Runners log after a new best evaluation)."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import calibration
+    rng = np.random.default_rng(2024)
+    out = {}
+    tmp = tempfile.mkdtemp(prefix="bdl_golden_calib_")
+    for name, (n, k, scale) in {"c10": (200, 10, 3.0), "c37": (64, 37, 1.5)}.items():
+        logits = (rng.standard_normal((n, k)) * scale).astype(np.float32)
+        labels = rng.integers(0, k, size=n)
+        labels[: n // 2] = logits[: n // 2].argmax(1)        # half of them confidently right
+        vlogits = (rng.standard_normal((n, k)) * scale).astype(np.float32)
+        vlabels = rng.integers(0, k, size=n)
+        vlabels[: n // 2] = vlogits[: n // 2].argmax(1)
+        out[f"{name}_logits"], out[f"{name}_labels"] = logits, labels
+        out[f"{name}_vlogits"], out[f"{name}_vlabels"] = vlogits, vlabels
+        for t in (1.0, 1.7):
+            out[f"{name}_analyze_T{t}"] = np.array(calibration.analyze(
+                labels, logits, num_bins=15, plot_save_path=os.path.join(tmp, "r.png"),
+                temperature=t), dtype=np.float64)
+        topt, ok = calibration.find_optimal_temperature(vlabels, vlogits,
+                                                        os.path.join(tmp, "t.png"))
+        out[f"{name}_topt"] = np.asarray(topt, dtype=np.float64)
+        out[f"{name}_topt_ok"] = np.bool_(ok)
+    return out
+
+
 def main():
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
     logging.basicConfig(level=logging.WARNING)
     methods = import_reference()
     torch.set_num_threads(1)
     only = os.environ.get("GOLDEN_ONLY")
+    if only == "calib":
+        np.savez_compressed(os.path.join(HERE, "calibration.npz"), **calibration_fixture())
+        print("wrote calibration.npz")
+        return
     if only == "ckpt":
         torch.set_num_threads(8)
         recs = {}
