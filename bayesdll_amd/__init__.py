@@ -7,7 +7,11 @@ Drop-in modules (same Runner/Model interfaces as the reference's methods/*.py):
     bayesdll_amd.sgld     SGLD            (methods/sgld.py, src/bayesdll/sgld.py)
     bayesdll_amd.adam_sghmc   Adam-preconditioned SGHMC          (methods/adam_sghmc.py)
     bayesdll_amd.adam_csghmc  cyclical Adam-preconditioned SGHMC (methods/adam_csghmc.py)
+    bayesdll_amd.csghmc_fs    cSGHMC with cold restarts + full-sample BMA (methods/csghmc_fs.py)
     bayesdll_amd.cyclical CyclicalSGMCMC  (methods/cyclical.py)
+    bayesdll_amd.calibration  ECE / MCE / NLL / temperature (calibration.py)
+    bayesdll_amd.chains   one chain per GPU; the cross-chain predictive (RCCL)
+    bayesdll_amd.run      command-line driver with the demos' flags (demo_mnist.py)
 
 The per-step update runs in hand-written HIP kernels for gfx950
 (bayesdll_amd/csrc/, one translation unit per kernel family) behind the C-ABI in include/bdl_sgmcmc.h,
