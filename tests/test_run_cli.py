@@ -50,3 +50,26 @@ def test_cli_end_to_end_tiny(method, tmp_path):
     assert len(logs) == 1 and logs[0].stat().st_size > 0
     if res is not None:  # the cyclical Runners return a results dict
         assert np.isfinite(res["losses_train"]).all()
+
+
+@pytest.mark.gpu
+def test_cli_vit_l_32_csghmc_config4(tmp_path):
+    """Config 4 at the Runner level: ViT-L/32 (306.5 M parameters) cSGHMC
+    through the CLI on Pets-shaped synthetic data — cyclical schedule, Welford
+    collection, cycle-end full-batch likelihoods + GMM weights, mixture
+    evaluation with fused posterior draws, calibration, checkpoints; every
+    loss finite and the per-cycle moments on the device."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    import numpy as np
+    from bayesdll_amd.run import main
+    res = main(["--method", "csghmc", "--dataset", "pets", "--backbone", "vit_l_32",
+                "--epochs", "2", "--num_cycles", "2", "--batch_size", "16", "--lr", "1e-4",
+                "--lr_head", "1e-2", "--train_size", "48", "--test_size", "16",
+                "--val_heldout", "0", "--log_dir", str(tmp_path),
+                "--hparams", "prior_sig=1.0,Ninflate=1.0,nd=0.01,burnin=0,momentum_decay=0.18,"
+                             "thin=1,bias=informative,nst=2"])
+    assert np.isfinite(res["losses_train"]).all() and np.isfinite(res["losses_test"]).all()
+    assert sorted(res["samples_per_cycle"]) == [1, 2]
+    ckpts = sorted(p.name for p in tmp_path.rglob("*_ckpt.pt"))
+    assert ckpts == ["1_ckpt.pt", "2_ckpt.pt"]
