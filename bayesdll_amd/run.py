@@ -182,8 +182,11 @@ def main(argv=None):
         net0 = create_backbone(args)
         for m in (net, net0):
             own = m.state_dict()
+            # networks/__init__.py:66-130: feature extractor from the file; the
+            # readout stays as created (random in net, zeroed in net0 below)
             m.load_state_dict({k: v for k, v in state.items()
-                               if k in own and own[k].shape == v.shape}, strict=False)
+                               if k in own and own[k].shape == v.shape
+                               and not k.startswith(m.readout_name + ".")}, strict=False)
         with torch.no_grad():
             for nm, p in net0.named_parameters():
                 if net0.readout_name in nm:
