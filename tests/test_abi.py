@@ -410,3 +410,14 @@ def test_algorithmic_bytes_per_element_match_design_table():
     assert alg_bytes_per_elem(args(L.ADAM_SGHMC, flags=mom), ad) == 48
     assert alg_bytes_per_elem(args(L.ADAM_SGHMC, flags=mom | L.FLAG_FIRST_STEP), ad) == 44
     assert alg_bytes_per_elem(args(L.ADAM_SGHMC, L.COLLECT_MEAN, flags=mom), ad) == 64
+
+
+def test_tools_and_examples_compile():
+    """The measurement scripts under tools/ stay importable-syntax clean."""
+    import glob
+    import py_compile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = glob.glob(os.path.join(root, "tools", "*.py"))
+    assert len(files) >= 15
+    for f in files:
+        py_compile.compile(f, doraise=True, cfile=os.devnull)
