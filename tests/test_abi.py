@@ -415,9 +415,9 @@ def test_algorithmic_bytes_per_element_match_design_table():
 def test_tools_and_examples_compile():
     """The measurement scripts under tools/ stay importable-syntax clean."""
     import glob
-    import py_compile
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     files = glob.glob(os.path.join(root, "tools", "*.py"))
     assert len(files) >= 15
     for f in files:
-        py_compile.compile(f, doraise=True, cfile=os.devnull)
+        with open(f) as fh:
+            compile(fh.read(), f, "exec")
