@@ -44,6 +44,15 @@ def default_graph():
     return os.environ.get("BDL_GRAPH", "0") not in ("", "0", "false", "False")
 
 
+def default_overlap():
+    """BDL_OVERLAP=1: launch the fused update per bucket of parameters as
+    their gradients complete, on a side stream, overlapping backward."""
+    return os.environ.get("BDL_OVERLAP", "0") not in ("", "0", "false", "False")
+
+
+OVERLAP_BUCKET_ELEMS = 1 << 24  # ~64 MB of fp32 per bucket
+
+
 def default_chain():
     """Chain id = process rank when torch.distributed is initialised."""
     from . import chains
@@ -68,6 +77,11 @@ class FusedModelBase(nn.Module):
         self.div_mode = None
         self.graph = default_graph()
         self._graphs = {}
+        self.overlap = default_overlap()
+        self._ovl = None          # per-backward bucket bookkeeping while overlapping
+        self._ovl_plan = None
+        self._ovl_hooks = None
+        self._side = None
         self._state = None
         self._state_net = None
 
@@ -108,6 +122,80 @@ class FusedModelBase(nn.Module):
         loss.backward()
         st.sync_grads()         # which tensors got a gradient, and where they live
         return loss, out
+
+    def can_overlap(self, st):
+        return (self.overlap and not self.graph and st.grad_mode == "tensor"
+                and self.noise_mode == "philox")
+
+    def forward_backward_overlapped(self, st, net, x, y, criterion, launch):
+        """Forward + backward with the fused update overlapped: the flat
+        vectors are cut into ~64 MB buckets of whole tensors
+        (FlatState.bucket_plan); when the last gradient of a bucket has been
+        accumulated (post-accumulate hook), `launch(bucket_state, start)`
+        enqueues that bucket's update on a side stream behind an event on the
+        backward's stream — every kernel that reads those parameters has been
+        enqueued before it — so the memory-bound sweep runs beside the
+        GEMM-bound backward of the layers below.  Same per-element arithmetic
+        and (with philox_offset = start // 4) the same noise as one launch:
+        the chain is bit-identical.  Buckets holding a parameter without a
+        gradient are launched after backward, with it skipped.  Philox noise
+        and "tensor" gradients only (can_overlap)."""
+        dev = st.device
+        if self._ovl_plan is None or self._ovl_plan[0] is not st:
+            plan = st.bucket_plan(OVERLAP_BUCKET_ELEMS)
+            owner = {}
+            for bi, (_, _, idx) in enumerate(plan):
+                for i in idx:
+                    owner[i] = bi
+            need = [sum(1 for i in idx if st.requires_grad[i]) for _, _, idx in plan]
+            self._ovl_plan = (st, plan, owner, need)
+            if self._ovl_hooks is not None:
+                for h in self._ovl_hooks:
+                    h.remove()
+            self._ovl_hooks = [p.register_post_accumulate_grad_hook(self._ovl_hook(i))
+                               for i, p in enumerate(st.params) if st.requires_grad[i]]
+            self._side = torch.cuda.Stream(dev)
+        _, plan, owner, need = self._ovl_plan
+        main = torch.cuda.current_stream(dev)
+        side = self._side
+
+        def fire(bi):
+            start, end, idx = plan[bi]
+            ptrs = [0 if st.params[i].grad is None else st.params[i].grad.data_ptr() for i in idx]
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                launch(st.bucket_state(plan[bi], ptrs), start)
+
+        out = net(x)
+        loss = criterion(out, y)
+        st.zero_grad()
+        self._ovl = {"pending": list(need), "done": [False] * len(plan), "fire": fire,
+                     "owner": owner}
+        try:
+            loss.backward()
+        finally:
+            ctx, self._ovl = self._ovl, None
+        for bi, d in enumerate(ctx["done"]):
+            if not d:
+                ctx["done"][bi] = True
+                fire(bi)
+        main.wait_stream(side)
+        st.sync_grads()  # which parameters got a gradient (has_grad / noise bookkeeping)
+        return loss, out
+
+    def _ovl_hook(self, i):
+        def hook(_p):
+            ctx = self._ovl
+            if ctx is None:
+                return
+            bi = ctx["owner"][i]
+            ctx["pending"][bi] -= 1
+            if ctx["pending"][bi] == 0 and not ctx["done"][bi]:
+                ctx["done"][bi] = True
+                ctx["fire"](bi)
+        return hook
 
     def _graphed_forward_backward(self, st, net, x, y, criterion):
         """Forward + loss + backward replayed from a captured HIP graph

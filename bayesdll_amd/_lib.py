@@ -24,7 +24,7 @@ COLLECT_NONE, COLLECT_WELFORD_INIT, COLLECT_WELFORD, COLLECT_MEAN_INIT, COLLECT_
 ATTR_HEAD, ATTR_PRIOR, ATTR_SKIP, ATTR_GUNALIGNED = 0x1, 0x2, 0x4, 0x8
 FLAG_FIRST_STEP, FLAG_RECIP_DIV, FLAG_MOMENTUM, FLAG_GRAD_READY = 0x1, 0x2, 0x4, 0x8
 VAR_GIVEN, VAR_RAW_MOMENTS, VAR_WELFORD = 0, 1, 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _fp = C.c_void_p
 
@@ -51,7 +51,7 @@ class StepArgs(C.Structure):
         ("collect_b", C.c_float), ("inv_sigma2", C.c_float), ("inv_n_data", C.c_float),
         ("inv_collect_a", C.c_float), ("inv_collect_b", C.c_float), ("pad1", C.c_float),
         ("seed", C.c_uint64), ("chain", C.c_uint64), ("step", C.c_uint64),
-        ("grad_base", _fp), ("nonfinite", _fp),
+        ("grad_base", _fp), ("nonfinite", _fp), ("philox_offset", C.c_uint64),
     ]
 
 

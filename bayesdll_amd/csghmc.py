@@ -58,6 +58,8 @@ class Runner:
             self.model.seed = int(args.seed)
         if getattr(args, "graph", None) is not None:
             self.model.graph = bool(args.graph)
+        if getattr(args, "overlap", None) is not None:
+            self.model.overlap = bool(args.overlap)
 
         # lr holder with the reference's two param groups (body, head)
         self.optimizer = torch.optim.SGD(
@@ -339,16 +341,28 @@ class Model(FusedModelBase):
         N = self.ND * Ninflate
         lr_body, lr_head = (lrs[0], lrs[0]) if len(lrs) == 1 else (lrs[0], lrs[1])
         st = self.state_for(net)
+        noise_scale = [nd * np.sqrt((2 * self.momentum_decay * lr)) / N for lr in (lr_body, lr_head)]
+        ckind, m1, m2, ca = (L.COLLECT_NONE, None, None, 1.0) if collect is None else collect
+        kw = dict(lrs=(lr_body, lr_head), noise_scale=noise_scale,
+                  one_minus_alpha=1 - self.momentum_decay, prior_sig=self.prior_sig,
+                  collect=ckind, collect_a=ca, seed=self.seed, chain=self.chain,
+                  step=self.step_count, div_mode=self.div_mode)
+        if self.can_overlap(st):
+            # update overlapped with backward, bucket by bucket (identical result)
+            sl = (lambda v, a, b: None if v is None else v[a:b])
+            nm = L.NOISE_PHILOX if should_sample else L.NOISE_NONE
+            loss, out = self.forward_backward_overlapped(
+                st, net, x, y, criterion,
+                lambda sub, start: K.sgmcmc_step(
+                    sub, L.CSGHMC, noise_mode=nm, mom1=sl(m1, start, start + sub.n),
+                    mom2=sl(m2, start, start + sub.n), philox_offset=start // 4, **kw))
+            self.step_count += 1
+            return loss.item(), out.detach()
         loss, out = self.forward_backward(st, net, x, y, criterion)
         # the reference draws randn_like on every step, even when the noise is
         # dropped (:766): the torch/external sources are advanced every step
         nmode = self.draw_noise(st)
-        noise_scale = [nd * np.sqrt((2 * self.momentum_decay * lr)) / N for lr in (lr_body, lr_head)]
-        ckind, m1, m2, ca = (L.COLLECT_NONE, None, None, 1.0) if collect is None else collect
-        K.sgmcmc_step(st, L.CSGHMC, lrs=(lr_body, lr_head), noise_scale=noise_scale,
-                      noise_mode=nmode if should_sample else L.NOISE_NONE,
-                      one_minus_alpha=1 - self.momentum_decay, prior_sig=self.prior_sig,
-                      collect=ckind, mom1=m1, mom2=m2, collect_a=ca, seed=self.seed,
-                      chain=self.chain, step=self.step_count, div_mode=self.div_mode)
+        K.sgmcmc_step(st, L.CSGHMC, noise_mode=nmode if should_sample else L.NOISE_NONE,
+                      mom1=m1, mom2=m2, **kw)
         self.step_count += 1
         return loss.item(), out.detach()

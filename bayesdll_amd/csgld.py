@@ -53,6 +53,8 @@ class Runner:
             self.model.seed = int(args.seed)
         if getattr(args, "graph", None) is not None:
             self.model.graph = bool(args.graph)
+        if getattr(args, "overlap", None) is not None:
+            self.model.overlap = bool(args.overlap)
         self.optimizer = torch.optim.SGD(
             [{"params": [p for pn, p in self.net.named_parameters()
                          if self.net.readout_name not in pn], "lr": args.lr},

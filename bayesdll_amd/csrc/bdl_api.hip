@@ -107,7 +107,7 @@ __device__ __forceinline__ double sqnorm_fast(const KArgs& a, const StepConst& c
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
-    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = philox_normal4((uint64_t)gi + a.goff, a.seed, a.chain, a.step);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float xt = th[u][j], xg = g[u][j], xv = 0.f;
@@ -154,7 +154,7 @@ __device__ __forceinline__ void sqnorm_body(const KArgs& a, double* __restrict__
         const f4v t0 = ld4(a.prior_mean, e, a.n);
         f4v ep = z;
         if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, a.n);
-        if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+        if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi + a.goff, a.seed, a.chain, a.step);
         for (int j = 0; j < 4; ++j) {
           if (e + j >= a.n) break;
           while (rr < a.nruns - 1 && run_end(rr) <= e + j) ++rr;
@@ -556,6 +556,7 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   a.step = s->step;
   a.clip = clip;
   a.nonfinite = s->nonfinite;
+  a.goff = s->philox_offset;
   a.inv_s2 = recip_or(s->inv_sigma2, s->sigma2);
   a.inv_nd = recip_or(s->inv_n_data, s->n_data);
   a.inv_ca = recip_or(s->inv_collect_a, s->collect_a);
@@ -668,6 +669,7 @@ int bdl_sgld_step_clipped(const bdl_step_args* s, float max_norm, void* workspac
   a.nruns = s->nruns;
   a.flags = s->flags;
   a.n = s->n;
+  a.goff = s->philox_offset;
   a.ns0 = s->noise_scale[0];
   a.ns1 = s->noise_scale[1];
   a.sigma2 = s->sigma2;
@@ -757,6 +759,7 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
   a.chain = s->chain;
   a.step = s->step;
   a.nonfinite = s->nonfinite;
+  a.goff = s->philox_offset;
   a.adam_m = ad->adam_m;
   a.adam_v = ad->adam_v;
   a.sgd_buf = ad->sgd_buf;

@@ -159,6 +159,7 @@ struct KArgs {
   uint64_t seed, chain, step;
   const float* __restrict__ clip;  // (total_norm, coef) from the clip finalize, or null
   int32_t* __restrict__ nonfinite;  // set to 1 if a written theta / grad value is not finite (or null)
+  uint64_t goff;  // Philox counter offset in float4 groups (a launch over a sub-range)
   // Adam-preconditioned SGHMC only (bdl_adam_step)
   float* __restrict__ adam_m;
   float* __restrict__ adam_v;
@@ -387,7 +388,7 @@ __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, i
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
     const int64_t e = gi * 4;
     if constexpr (NOISE == BDL_NOISE_PHILOX && !GR)
-      ep[u] = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+      ep[u] = philox_normal4((uint64_t)gi + a.goff, a.seed, a.chain, a.step);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float xt = th[u][j], xg = g[u][j], xv = v[u][j], x1 = m1[u][j], x2 = m2[u][j];
@@ -484,7 +485,7 @@ __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, i
     if (T::kMom || (METHOD == BDL_SGLD && c.sgd_mom_read)) v = ld4(a.mom, e, n);
     if (T::kReadPrior) t0 = ld4(a.prior_mean, e, n);
     if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, n);
-    if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+    if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi + a.goff, a.seed, a.chain, a.step);
     if (T::kReadMoments) {
       m1 = ld4(a.mom1, e, n);
       if (c.has_m2) m2 = ld4(a.mom2, e, n);
@@ -656,7 +657,7 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
   for (int u = 0; u < U; ++u) {
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
     const int64_t e = gi * 4;
-    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = philox_normal4((uint64_t)gi + a.goff, a.seed, a.chain, a.step);
     StepConst cc;  // collect_core only reads inv_ca / inv_cb
     cc.inv_ca = c.inv_ca;
     cc.inv_cb = c.inv_cb;
@@ -713,7 +714,7 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
     f4v buf = z, ep = z, m1 = z, m2 = z;
     if (!GRADONLY && c.sgd_mom_read) buf = ld4(a.sgd_buf, e, n);
     if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, n);
-    if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+    if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi + a.goff, a.seed, a.chain, a.step);
     if (COLLECT == BDL_COLLECT_MEAN) {
       m1 = ld4(a.mom1, e, n);
       if (c.has_m2) m2 = ld4(a.mom2, e, n);

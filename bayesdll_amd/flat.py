@@ -446,6 +446,54 @@ class FlatState:
             self.nonfinite.zero_()
         return bad
 
+    # ------------------------------------------------- buckets (overlap)
+    def bucket_plan(self, target_elems):
+        """Contiguous buckets of whole tensors, each about `target_elems`
+        long, cut only at flat offsets that are multiples of 4 (a float4 group
+        never spans two buckets): [(start, end, tensor indices), ...]."""
+        out, start, cur = [], 0, []
+        for i, (o, k) in enumerate(zip(self.offsets, self.numels)):
+            cur.append(i)
+            end = o + k
+            if end - start >= target_elems and end % 4 == 0:
+                out.append((start, end, tuple(cur)))
+                start, cur = end, []
+        if cur:
+            out.append((start, self.n, tuple(cur)))
+        return out
+
+    def bucket_state(self, bucket, ptrs):
+        """A launchable view of one bucket: every vector sliced to
+        [start, end), a per-tensor run table with ends relative to `start`
+        and gradient bases shifted so local element e reads
+        ptrs[j] + 4*(start + e - offset_j); launch it with
+        philox_offset = start // 4 for the whole-vector noise."""
+        from types import SimpleNamespace
+        start, end, idx = bucket
+        key = (start, tuple(ptrs))
+        tab = self._grad_tables.get(key)
+        if tab is None:
+            nt = len(idx)
+            host = torch.empty(3 * nt, dtype=torch.int64).pin_memory()
+            h = host.numpy()
+            for j, (i, ptr) in enumerate(zip(idx, ptrs)):
+                o, k = self.offsets[i], self.numels[i]
+                at = self.attrs[i] | (L.ATTR_SKIP if not ptr else 0)
+                base = ptr - 4 * o + 4 * start if ptr else 0
+                if ptr and base % 16:
+                    at |= L.ATTR_GUNALIGNED
+                h[2 * j], h[2 * j + 1], h[2 * nt + j] = o + k - start, at, base
+            dev = host.to(self.device, non_blocking=True)
+            tab = (dev[:2 * nt].view(nt, 2), nt, dev[2 * nt:])
+            if len(self._grad_tables) >= 4 * GRAD_TABLE_CACHE:
+                self._grad_tables.pop(next(iter(self._grad_tables)))
+            self._grad_tables[key] = tab
+        sl = (lambda v: None if v is None else v[start:end])
+        return SimpleNamespace(theta=self.theta[start:end], grad=None, gbase=tab[2], runs=tab[0],
+                               nruns=tab[1], mom=sl(self.mom), prior=sl(self.prior), noise=None,
+                               n=end - start, device=self.device, nonfinite=self.nonfinite,
+                               extra={k: v[start:end] for k, v in self.extra.items()}, timer=None)
+
     def grad_table(self):
         """The run / gradient-base selection of the current step (to reuse
         when the same gradient tensors are produced again, e.g. graph replay)."""

@@ -38,7 +38,7 @@ def _step_args(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1
                prior_sig=0.0, sigma2=1.0, n_data=1.0, mu=0.0, first_step=False,
                momentum=False, collect=L.COLLECT_NONE, mom1=None, mom2=None, collect_a=1.0,
                collect_b=1.0, seed=0, chain=0, step=0, div_mode=None, noise=None, grad_ready=False,
-               mom_buf=None):
+               mom_buf=None, philox_offset=0):
     a = L.StepArgs()
     a.theta = state.theta.data_ptr()
     g = getattr(state, "grad", None)
@@ -76,6 +76,7 @@ def _step_args(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1
     a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     a.chain = int(chain) & 0xFFFFFFFFFFFFFFFF
     a.step = int(step) & 0xFFFFFFFFFFFFFFFF
+    a.philox_offset = int(philox_offset)
     return a
 
 
@@ -160,7 +161,7 @@ def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps,
               momentum_decay, nd, temperature=1.0, grad_is_mom=False, lrs, noise_mode,
               sigma2, n_data, mu=0.0, first_step=False, momentum=False, collect=L.COLLECT_NONE,
               mom1=None, mom2=None, collect_a=1.0, collect_b=1.0, seed=0, chain=0, step=0,
-              div_mode=None, noise=None):
+              div_mode=None, noise=None, philox_offset=0):
     """One fused Adam-preconditioned SGHMC step (methods/adam_sghmc.py:500-553,
     adam_csghmc.py:812-860) + SGD step.  The host-side scalars are formed in
     float64 exactly as the reference's Python does (1 - beta1, 1 - beta1**t,
@@ -169,7 +170,7 @@ def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps,
                    one_minus_alpha=1 - momentum_decay, sigma2=sigma2, n_data=n_data, mu=mu,
                    first_step=first_step, momentum=momentum, collect=collect, mom1=mom1,
                    mom2=mom2, collect_a=collect_a, collect_b=collect_b, seed=seed, chain=chain,
-                   step=step, div_mode=div_mode, noise=noise)
+                   step=step, div_mode=div_mode, noise=noise, philox_offset=philox_offset)
     ad = L.AdamArgs()
     ad.adam_m = adam_m.data_ptr()
     ad.adam_v = adam_v.data_ptr()

@@ -101,6 +101,8 @@ def build_parser():
     # MI355X path options
     ap.add_argument("--noise_mode", type=str, default="philox", choices=["philox", "torch"])
     ap.add_argument("--graph", action="store_true", help="replay forward/backward from a HIP graph")
+    ap.add_argument("--overlap", action="store_true",
+                    help="overlap the fused update with backward, bucket by bucket (cSGHMC)")
     ap.add_argument("--resume_state", action="store_true",
                     help="checkpoints carry what an exact resume needs")
     return ap

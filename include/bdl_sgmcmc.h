@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define BDL_ABI_VERSION 4
+#define BDL_ABI_VERSION 5
 
 typedef enum bdl_status {
   BDL_OK = 0,
@@ -184,6 +184,11 @@ typedef struct bdl_step_args {
    * +-Inf.  Never written on a healthy chain; the host reads it when it likes
    * (e.g. once per epoch), so the guard adds no synchronisation. */
   int32_t* nonfinite;
+  /* Philox counter offset, in float4 groups: a launch over the sub-range
+   * [4*philox_offset, 4*philox_offset + n) of a chain's flat vectors (all
+   * pointers and the run table shifted to it) draws exactly the noise the
+   * whole-vector launch draws there.  0 for whole-vector launches. */
+  uint64_t philox_offset;
 } bdl_step_args;
 
 /* Extra state and scalars of the Adam-preconditioned SGHMC step.  Per element,

@@ -349,3 +349,104 @@ def test_step_timing_log(caplog):
         os.environ.pop("BDL_STEP_TIMING", None)
     lines = [m for m in caplog.messages if "fused update:" in m]
     assert len(lines) == 2 and "4 launches" in lines[0] and "GB/s algorithmic" in lines[0]
+
+
+def test_philox_offset_subrange_launches_equal_one_launch():
+    """bdl_step_args.philox_offset: launching the cSGHMC step bucket by bucket
+    over sub-ranges (FlatState.bucket_state, offsets multiples of 4) gives,
+    bit for bit, the whole-vector launch — Philox noise and Welford collection
+    included."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.flat import FlatState
+    from bayesdll_amd.shapes import segments
+    segs, readout = segments("resnet101", 37)
+    sts = []
+    for _ in range(2):
+        st = FlatState.from_segments(segs, readout, device=DEV)
+        g = torch.Generator(device=DEV).manual_seed(7)
+        st.theta.normal_(0, 0.02, generator=g)
+        st.grad.normal_(0, 1e-3, generator=g)
+        st.mom.normal_(0, 1e-4, generator=g)
+        st.flatg = st.grad  # keep the storage the per-tensor views read
+        st.use_tensor_grads([st.grad[o:o + k] for o, k in zip(st.offsets, st.numels)])
+        sts.append(st)
+    m1 = [torch.full((sts[0].n,), 0.01, device=DEV) for _ in range(2)]
+    m2 = [torch.full((sts[0].n,), 1e-4, device=DEV) for _ in range(2)]
+    kw = dict(lrs=(1e-4, 1e-2), noise_scale=(1e-3, 2e-3), noise_mode=L.NOISE_PHILOX,
+              one_minus_alpha=0.82, prior_sig=1.0, collect=L.COLLECT_WELFORD, collect_a=3.0,
+              seed=5, chain=2, step=11)
+    K.sgmcmc_step(sts[0], L.CSGHMC, mom1=m1[0], mom2=m2[0], **kw)
+    st = sts[1]
+    plan = st.bucket_plan(1 << 20)
+    assert len(plan) > 10 and all(b[0] % 4 == 0 for b in plan)
+    grads = [st.flatg[o:o + k] for o, k in zip(st.offsets, st.numels)]
+    for b in plan:
+        sub = st.bucket_state(b, [grads[i].data_ptr() for i in b[2]])
+        K.sgmcmc_step(sub, L.CSGHMC, mom1=m1[1][b[0]:b[1]], mom2=m2[1][b[0]:b[1]],
+                      philox_offset=b[0] // 4, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(sts[0].theta, sts[1].theta) and torch.equal(sts[0].mom, sts[1].mom)
+    assert torch.equal(m1[0], m1[1]) and torch.equal(m2[0], m2[1])
+
+
+def test_overlapped_update_equals_one_launch(monkeypatch):
+    """BDL_OVERLAP / Model.overlap: the cSGHMC update launched per bucket from
+    post-accumulate hooks on a side stream, overlapping backward, gives the
+    sequential chain bit for bit (explore and sample steps, Welford collects,
+    a parameter without a gradient in one step)."""
+    import bayesdll_amd._base as B
+    import bayesdll_amd.csghmc as csghmc
+    from fakenet import MLP, init_vector, synthetic_mnist
+    monkeypatch.setattr(B, "OVERLAP_BUCKET_ELEMS", 1 << 18)  # several buckets on an MLP
+    n = 2797010
+    init = torch.tensor(init_vector(91, n, 0.03))
+    data = synthetic_mnist(92, 256, 64, device=DEV)
+    crit = torch.nn.CrossEntropyLoss()
+
+    class Net(MLP):
+        def __init__(self):
+            super().__init__()
+            self.extra = torch.nn.Linear(4, 4)   # used on some steps only
+            self.use_extra = True
+
+        def forward(self, x):
+            out = super().forward(x)
+            if self.use_extra:
+                out = out + 0.0 * self.extra(torch.ones(1, 4, device=x.device)).sum()
+            return out
+
+    def run(overlap):
+        torch.manual_seed(0)
+        net = Net()
+        with torch.no_grad():
+            torch.nn.utils.vector_to_parameters(
+                torch.cat([init, torch.zeros(20)]), net.parameters())
+        net = net.to(DEV)
+        model = csghmc.Model(30000.0, prior_sig=1.0, momentum_decay=0.18)
+        model.noise_mode, model.seed, model.overlap = "philox", 3, overlap
+        st = None
+        m1 = m2 = None
+        for ep in range(2):
+            for k, (x, y) in enumerate(data):
+                net.use_extra = k != 2
+                coll = None
+                if k == 1:
+                    st = model.flat
+                    if m1 is None:
+                        m1 = torch.empty(st.n, device=DEV)
+                        m2 = torch.empty(st.n, device=DEV)
+                        coll = (1, m1, m2, 1.0)        # COLLECT_WELFORD_INIT
+                    else:
+                        coll = (2, m1, m2, 2.0)        # COLLECT_WELFORD
+                model(x, y, net, None, crit, [1e-2, 2e-2], 1.0, 0.5, should_sample=k % 2 == 1,
+                      collect=coll)
+        torch.cuda.synchronize()
+        return model, m1, m2
+
+    mo, m1o, m2o = run(True)
+    ms, m1s, m2s = run(False)
+    assert mo._ovl_plan is not None and len(mo._ovl_plan[1]) >= 4
+    assert torch.equal(mo.flat.theta, ms.flat.theta)
+    assert torch.equal(mo.flat.mom, ms.flat.mom)
+    assert torch.equal(m1o, m1s) and torch.equal(m2o, m2s)

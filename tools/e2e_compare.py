@@ -38,11 +38,12 @@ def main():
     crit = torch.nn.CrossEntropyLoss()
     lrs = [1e-4, 1e-2]
     res = {}
-    for mode in ("reference_torch_ops", "fused", "fused_graph"):
+    for mode in ("reference_torch_ops", "fused", "fused_graph", "fused_overlap"):
         torch.manual_seed(0)
         net = backbone(name, classes).to(dev)
         model = csghmc.Model(ND=1840, prior_sig=1.0, momentum_decay=0.18)
         model.graph = mode == "fused_graph"  # forward + backward from a captured HIP graph
+        model.overlap = mode == "fused_overlap"  # update per bucket, overlapping backward
         moms = {n: torch.zeros_like(p) for n, p in net.named_parameters()}
         fwdbwd = upd = 0.0
         for k in range(steps + 3):
@@ -63,7 +64,7 @@ def main():
         res[mode] = (time.perf_counter() - t0) / steps * 1e3
         # update-only timing
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        if mode == "fused_graph":
+        if mode in ("fused_graph", "fused_overlap"):
             pass
         elif mode == "fused":
             from bayesdll_amd import _lib as L
@@ -82,7 +83,7 @@ def main():
                 reference_update(net, moms, lrs, 1.0, 0.18, 1840.0, 0.01, True)
             e1.record()
         torch.cuda.synchronize()
-        if mode != "fused_graph":
+        if mode not in ("fused_graph", "fused_overlap"):
             res[mode + "_update_only"] = e0.elapsed_time(e1) / steps
         del net, model, moms
         torch.cuda.empty_cache()
