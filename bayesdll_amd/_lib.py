@@ -24,7 +24,7 @@ COLLECT_NONE, COLLECT_WELFORD_INIT, COLLECT_WELFORD, COLLECT_MEAN_INIT, COLLECT_
 ATTR_HEAD, ATTR_PRIOR, ATTR_SKIP, ATTR_GUNALIGNED = 0x1, 0x2, 0x4, 0x8
 FLAG_FIRST_STEP, FLAG_RECIP_DIV, FLAG_MOMENTUM, FLAG_GRAD_READY = 0x1, 0x2, 0x4, 0x8
 VAR_GIVEN, VAR_RAW_MOMENTS, VAR_WELFORD = 0, 1, 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _fp = C.c_void_p
 
@@ -52,6 +52,7 @@ class StepArgs(C.Structure):
         ("inv_collect_a", C.c_float), ("inv_collect_b", C.c_float), ("pad1", C.c_float),
         ("seed", C.c_uint64), ("chain", C.c_uint64), ("step", C.c_uint64),
         ("grad_base", _fp), ("nonfinite", _fp), ("philox_offset", C.c_uint64),
+        ("chain_groups", C.c_uint64),
     ]
 
 
@@ -77,7 +78,7 @@ class SampleArgs(C.Structure):
                 ("var_mode", C.c_int32), ("noise_mode", C.c_int32), ("ratio", C.c_float),
                 ("var_floor", C.c_float), ("inv_ratio", C.c_float), ("pad", C.c_float),
                 ("seed", C.c_uint64), ("chain", C.c_uint64),
-                ("step", C.c_uint64)]
+                ("step", C.c_uint64), ("chain_groups", C.c_uint64)]
 
 
 EXPORTS = {

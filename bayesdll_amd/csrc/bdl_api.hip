@@ -107,7 +107,7 @@ __device__ __forceinline__ double sqnorm_fast(const KArgs& a, const StepConst& c
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
-    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = philox_normal4((uint64_t)gi + a.goff, a.seed, a.chain, a.step);
+    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = step_noise4(a, gi);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float xt = th[u][j], xg = g[u][j], xv = 0.f;
@@ -154,7 +154,7 @@ __device__ __forceinline__ void sqnorm_body(const KArgs& a, double* __restrict__
         const f4v t0 = ld4(a.prior_mean, e, a.n);
         f4v ep = z;
         if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, a.n);
-        if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi + a.goff, a.seed, a.chain, a.step);
+        if (NOISE == BDL_NOISE_PHILOX) ep = step_noise4(a, gi);
         for (int j = 0; j < 4; ++j) {
           if (e + j >= a.n) break;
           while (rr < a.nruns - 1 && run_end(rr) <= e + j) ++rr;
@@ -329,6 +329,7 @@ struct SArgs {
   int32_t var_mode, noise_mode;
   float ratio, var_floor, inv_ratio;
   uint64_t seed, chain, step;
+  uint32_t cgroups;  // stacked chains: float4 groups per chain (0 = one chain)
 };
 
 // theta_s = m1 + sqrt(clamp(var, floor)) * eps.  VAR: where the variance
@@ -336,6 +337,17 @@ struct SArgs {
 // cycle, csghmc.py:456-458); RECIP: Welford M2 * fl(1/(n-1)) as torch on the
 // device; NOISE: buffer or in-register Philox.  Same sweep shape as the
 // moments kernel.
+// Philox draw for group gi (stacked chains as in step_noise4).
+__device__ __forceinline__ f4v sample_noise4(const SArgs& a, int64_t gi) {
+  uint64_t g = (uint64_t)gi, c = a.chain;
+  if (a.cgroups) {
+    const uint32_t k = (uint32_t)g / a.cgroups;
+    g -= (uint64_t)k * a.cgroups;
+    c += k;
+  }
+  return philox_normal4(g, a.seed, c, a.step);
+}
+
 template <int VAR, bool M2, bool RECIP>
 __device__ __forceinline__ float sample_var(const SArgs& a, float mj, float qj) {
   float var;
@@ -379,7 +391,7 @@ __global__ __launch_bounds__(kBlock) void bdl_sample_kernel(const SArgs a) {
       const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
       const int64_t e = gi * 4;
       if constexpr (NOISE == BDL_NOISE_PHILOX)
-        ep[u] = philox_normal4((uint64_t)gi, a.seed, a.chain, a.step);
+        ep[u] = sample_noise4(a, gi);
       f4v o;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -481,6 +493,11 @@ int check_runs_and_grad(const bdl_step_args* s, const char* what) {
     return fail(BDL_ERR_ALIGN, std::string(what) + ": grad not 16-B aligned");
   if (s->grad_base && (reinterpret_cast<uintptr_t>(s->grad_base) & 7u))
     return fail(BDL_ERR_ALIGN, std::string(what) + ": grad_base not 8-B aligned");
+  if (s->chain_groups &&
+      (s->chain_groups > 0xFFFFFFFFull ||
+       (uint64_t)((s->n + 3) / 4) + s->philox_offset > 0xFFFFFFFFull))
+    return fail(BDL_ERR_ARG, std::string(what) + ": stacked chains need every float4 group "
+                "index below 2^32 (chain_groups, n / 4 + philox_offset)");
   return BDL_OK;
 }
 
@@ -557,6 +574,7 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   a.clip = clip;
   a.nonfinite = s->nonfinite;
   a.goff = s->philox_offset;
+  a.cgroups = (uint32_t)s->chain_groups;
   a.inv_s2 = recip_or(s->inv_sigma2, s->sigma2);
   a.inv_nd = recip_or(s->inv_n_data, s->n_data);
   a.inv_ca = recip_or(s->inv_collect_a, s->collect_a);
@@ -670,6 +688,7 @@ int bdl_sgld_step_clipped(const bdl_step_args* s, float max_norm, void* workspac
   a.flags = s->flags;
   a.n = s->n;
   a.goff = s->philox_offset;
+  a.cgroups = (uint32_t)s->chain_groups;
   a.ns0 = s->noise_scale[0];
   a.ns1 = s->noise_scale[1];
   a.sigma2 = s->sigma2;
@@ -760,6 +779,7 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
   a.step = s->step;
   a.nonfinite = s->nonfinite;
   a.goff = s->philox_offset;
+  a.cgroups = (uint32_t)s->chain_groups;
   a.adam_m = ad->adam_m;
   a.adam_v = ad->adam_v;
   a.sgd_buf = ad->sgd_buf;
@@ -828,8 +848,13 @@ int bdl_posterior_sample(const bdl_sample_args* s, void* stream) {
   const void* ptrs[] = {s->out, s->mom1, s->mom2, s->noise};
   for (const void* p : ptrs)
     if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_posterior_sample: vector not 16-B aligned");
+  if (s->chain_groups &&
+      (s->chain_groups > 0xFFFFFFFFull || (uint64_t)((s->n + 3) / 4) > 0xFFFFFFFFull))
+    return fail(BDL_ERR_ARG, "bdl_posterior_sample: stacked chains need every float4 group "
+                "index below 2^32");
   SArgs a{s->out, s->mom1, s->mom2, s->noise, s->n, s->var_mode, s->noise_mode,
-          s->ratio, s->var_floor, s->inv_ratio, s->seed, s->chain, s->step};
+          s->ratio, s->var_floor, s->inv_ratio, s->seed, s->chain, s->step,
+          (uint32_t)s->chain_groups};
   hipLaunchKernelGGL(pick_sample(s->var_mode, s->mom2 != nullptr, s->inv_ratio != 0.0f,
                                  s->noise_mode),
                      dim3(grid_sample((s->n + 3) / 4)), dim3(kBlock), 0,

@@ -160,6 +160,7 @@ struct KArgs {
   const float* __restrict__ clip;  // (total_norm, coef) from the clip finalize, or null
   int32_t* __restrict__ nonfinite;  // set to 1 if a written theta / grad value is not finite (or null)
   uint64_t goff;  // Philox counter offset in float4 groups (a launch over a sub-range)
+  uint32_t cgroups;  // stacked chains: float4 groups per chain (0 = one chain)
   // Adam-preconditioned SGHMC only (bdl_adam_step)
   float* __restrict__ adam_m;
   float* __restrict__ adam_v;
@@ -168,6 +169,21 @@ struct KArgs {
   // scalar-divisor reciprocals for BDL_FLAG_RECIP_DIV (host-rounded fl32(1/s64))
   float inv_s2, inv_nd, inv_ca, inv_cb, inv_temp, inv_bc1, inv_bc2;
 };
+
+// The Philox draw for float4 group gi of a launch.  The counter is the group
+// index within its chain: with stacked chains (cgroups > 0, chain k's elements
+// at [4*cgroups*k, 4*cgroups*(k+1))) chain k is keyed chain + k and draws what
+// a one-chain launch with that chain id draws.  The host keeps every group
+// index below 2^32 in that mode, so the split is a 32-bit division.
+__device__ __forceinline__ f4v step_noise4(const KArgs& a, int64_t gi) {
+  uint64_t g = (uint64_t)gi + a.goff, c = a.chain;
+  if (a.cgroups) {
+    const uint32_t k = (uint32_t)g / a.cgroups;
+    g -= (uint64_t)k * a.cgroups;
+    c += k;
+  }
+  return philox_normal4(g, a.seed, c, a.step);
+}
 
 // fl32(1/s64) from the caller, or 1/fl32(s) when it left the field 0
 inline float recip_or(float inv, float s) { return inv != 0.0f ? inv : 1.0f / s; }
@@ -388,7 +404,7 @@ __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, i
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
     const int64_t e = gi * 4;
     if constexpr (NOISE == BDL_NOISE_PHILOX && !GR)
-      ep[u] = philox_normal4((uint64_t)gi + a.goff, a.seed, a.chain, a.step);
+      ep[u] = step_noise4(a, gi);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float xt = th[u][j], xg = g[u][j], xv = v[u][j], x1 = m1[u][j], x2 = m2[u][j];
@@ -485,7 +501,7 @@ __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, i
     if (T::kMom || (METHOD == BDL_SGLD && c.sgd_mom_read)) v = ld4(a.mom, e, n);
     if (T::kReadPrior) t0 = ld4(a.prior_mean, e, n);
     if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, n);
-    if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi + a.goff, a.seed, a.chain, a.step);
+    if (NOISE == BDL_NOISE_PHILOX) ep = step_noise4(a, gi);
     if (T::kReadMoments) {
       m1 = ld4(a.mom1, e, n);
       if (c.has_m2) m2 = ld4(a.mom2, e, n);
@@ -657,7 +673,7 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
   for (int u = 0; u < U; ++u) {
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
     const int64_t e = gi * 4;
-    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = philox_normal4((uint64_t)gi + a.goff, a.seed, a.chain, a.step);
+    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = step_noise4(a, gi);
     StepConst cc;  // collect_core only reads inv_ca / inv_cb
     cc.inv_ca = c.inv_ca;
     cc.inv_cb = c.inv_cb;
@@ -714,7 +730,7 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
     f4v buf = z, ep = z, m1 = z, m2 = z;
     if (!GRADONLY && c.sgd_mom_read) buf = ld4(a.sgd_buf, e, n);
     if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, n);
-    if (NOISE == BDL_NOISE_PHILOX) ep = philox_normal4((uint64_t)gi + a.goff, a.seed, a.chain, a.step);
+    if (NOISE == BDL_NOISE_PHILOX) ep = step_noise4(a, gi);
     if (COLLECT == BDL_COLLECT_MEAN) {
       m1 = ld4(a.mom1, e, n);
       if (c.has_m2) m2 = ld4(a.mom2, e, n);

@@ -77,6 +77,7 @@ def _step_args(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1
     a.chain = int(chain) & 0xFFFFFFFFFFFFFFFF
     a.step = int(step) & 0xFFFFFFFFFFFFFFFF
     a.philox_offset = int(philox_offset)
+    a.chain_groups = int(getattr(state, "chain_groups", 0))  # stacked chains (StackedState)
     return a
 
 
@@ -230,8 +231,9 @@ def moments_update(theta, mom1, mom2, collect, collect_a=1.0, collect_b=1.0, div
 
 
 def posterior_sample(out, mom1, mom2, *, var_mode, ratio=1.0, var_floor=1e-12, noise=None,
-                     seed=0, chain=0, step=0, div_mode=None):
-    """out = mom1 + sqrt(clamp(var(mom1, mom2), var_floor)) * eps (eps: buffer or Philox)."""
+                     seed=0, chain=0, step=0, div_mode=None, chain_groups=0):
+    """out = mom1 + sqrt(clamp(var(mom1, mom2), var_floor)) * eps (eps: buffer or Philox;
+    chain_groups > 0: stacked chains keyed chain + k, bdl_sample_args.chain_groups)."""
     L.require_hip(out, "out")
     a = L.SampleArgs()
     a.out, a.mom1 = out.data_ptr(), mom1.data_ptr()
@@ -245,6 +247,7 @@ def posterior_sample(out, mom1, mom2, *, var_mode, ratio=1.0, var_floor=1e-12, n
     # WELFORD M2 / (n-1): torch-on-GPU multiplies by the reciprocal
     a.inv_ratio = _inv(ratio) if _div_flag(div_mode) else 0.0
     a.seed, a.chain, a.step = int(seed), int(chain), int(step) & 0xFFFFFFFFFFFFFFFF
+    a.chain_groups = int(chain_groups)
     L.check(L.lib().bdl_posterior_sample(a, L.current_stream_handle(out.device)),
             "bdl_posterior_sample")
 

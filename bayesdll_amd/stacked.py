@@ -1,0 +1,403 @@
+"""Stacked chains: K independent cSGHMC chains of one network on one device.
+
+The reference runs one chain per process (methods/csghmc.py:41); its own
+recipe for more chains is more processes.  On an MI355X a small network
+leaves the device idle between launches, so K chains here share every
+launch instead:
+
+  * the K chains' flat vectors are stacked chain-major in one buffer
+    (`theta[k]` = parameters_to_vector of chain k, padded to a multiple of 4
+    elements so every chain starts on a float4 group);
+  * forward and backward run once for all chains, `torch.func.vmap` over
+    `functional_call` with the chains' parameters as strided views of the
+    stacked theta (the data batch shared, or one batch per chain);
+  * ONE fused update launch (`bdl_sgmcmc_step` with `chain_groups`, ABI v6)
+    covers all chains, reading each chain's gradient in place from the vmapped
+    gradient tensors through the per-run base table (one run per chain and
+    tensor), with the Welford collect of methods/csghmc.py:327-345 fused.
+
+Chain k draws the Philox noise of a one-chain sampler with chain id
+`chain0 + k` (same seed, same step keys): its update equals the one-chain
+update bit for bit given the same gradient (tests/test_gpu_stacked.py).  The
+gradients come from batched GEMMs, so a stacked chain agrees with a separately
+run chain to rounding, not bitwise.
+
+Scope: cSGHMC (the north-star sampler) with the reference's cyclical
+schedule, thinning and per-cycle Welford moments; the predictive averages
+probabilities uniformly over chains and (nst posterior draws of) collected
+cycles.  Networks with BatchNorm running statistics are refused (vmap cannot
+update shared buffers per chain), and every trainable parameter must take part
+in the forward pass (torch.func returns zeros, not None, for unused inputs).
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch.func import functional_call, grad_and_value, vmap
+
+from . import _lib as L
+from . import kernels as K
+from ._runner import EVAL_STEP_BASE
+from .cyclical import CyclicalSGMCMC
+from .flat import MAX_TENSOR_RUNS, build_runs, segment_attrs
+
+
+class StackedState:
+    """K chains' flat cSGHMC state of one network, stacked chain-major.
+
+    theta2d / mom2d are [K, stride] (stride = n rounded up to 4); `params`
+    maps every parameter name to its [K, *shape] strided view of theta2d.  The
+    launchable attributes (theta, grad / gbase, mom, runs, nruns, n,
+    chain_groups, nonfinite) are what kernels._step_args reads."""
+
+    def __init__(self, net, K_, *, readout_name=None, bias="informative", init="copy",
+                 seed=0, need_mom=True):
+        import torch.nn as nn
+        if K_ < 1:
+            raise ValueError("StackedState: K must be >= 1")
+        for m in net.modules():
+            if isinstance(m, nn.modules.batchnorm._BatchNorm) and m.track_running_stats:
+                raise ValueError("StackedState: BatchNorm running statistics cannot be stacked "
+                                 "(use track_running_stats=False or one chain per process)")
+        named = list(net.named_parameters())
+        if not named:
+            raise ValueError("StackedState: the network has no parameters")
+        dev = named[0][1].device
+        for nm, p in named:
+            L.require_hip(p.data, f"parameter {nm!r}")
+        self.K = int(K_)
+        self.device = dev
+        self.names = [nm for nm, _ in named]
+        self.shapes = [tuple(p.shape) for _, p in named]
+        self.numels = [p.numel() for _, p in named]
+        self.offsets = np.concatenate([[0], np.cumsum(self.numels)[:-1]]).astype(np.int64).tolist()
+        self.n1 = int(sum(self.numels))
+        self.stride = (self.n1 + 3) // 4 * 4
+        self.n = self.K * self.stride
+        self.chain_groups = self.stride // 4
+        if (self.n + 3) // 4 >= 1 << 32:
+            raise ValueError("StackedState: K * n too large for stacked Philox keys")
+        self.requires_grad = [p.requires_grad for _, p in named]
+        self.readout_name = readout_name if readout_name is not None else getattr(
+            net, "readout_name", None)
+        self.attrs = segment_attrs(self.names, self.readout_name, bias, self.requires_grad)
+
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.theta2d = torch.zeros(self.K, self.stride, **f32)
+        with torch.no_grad():
+            src = torch.cat([p.detach().reshape(-1).float() for _, p in named])
+            self.theta2d[:, :self.n1].copy_(src)
+            if init == "reinit":
+                import copy
+                from ._runner import reinit_network
+                tmp = copy.deepcopy(net)
+                for k in range(self.K):
+                    with torch.random.fork_rng(devices=[dev] if dev.type == "cuda" else []):
+                        torch.manual_seed(int(seed) + k)
+                        reinit_network(tmp)
+                    self.theta2d[k, :self.n1].copy_(
+                        torch.cat([p.detach().reshape(-1) for p in tmp.parameters()]))
+            elif init != "copy":
+                raise ValueError("StackedState: init must be 'copy' or 'reinit'")
+        self.theta = self.theta2d.view(-1)
+        self.mom2d = torch.zeros(self.K, self.stride, **f32) if need_mom else None
+        self.mom = None if self.mom2d is None else self.mom2d.view(-1)
+        self.prior, self.noise = None, None
+        self.nonfinite = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.params = {nm: self.theta2d[:, o:o + k].view(self.K, *s)
+                       for nm, o, k, s in zip(self.names, self.offsets, self.numels, self.shapes)}
+        # gradient source: per-run bases into the vmapped gradient tensors
+        # ("tensor"), or a stacked gradient vector the gradients are copied into
+        # ("flat", when K x tensors runs would not fit the LDS run table)
+        gap = 1 if self.stride > self.n1 else 0
+        self.grad_mode = "tensor" if self.K * (len(self.names) + gap) <= MAX_TENSOR_RUNS else "flat"
+        self.grad, self.gbase, self._tables = None, None, {}
+        if self.grad_mode == "flat":
+            self.grad2d = torch.zeros(self.K, self.stride, **f32)
+            self.grad = self.grad2d.view(-1)
+            offs, nums, ats = [], [], []
+            for k in range(self.K):
+                for o, kk, a in zip(self.offsets, self.numels, self.attrs):
+                    offs.append(k * self.stride + o)
+                    nums.append(kk)
+                    ats.append(a)
+            self.runs = build_runs(offs, nums, ats, self.n).to(dev)
+            self.nruns = int(self.runs.shape[0])
+        else:
+            self.runs, self.nruns = None, 0
+        self.timer = None
+        self.extra = {}
+
+    def chain_vector(self, k):
+        """parameters_to_vector of chain k (a view)."""
+        return self.theta2d[k, :self.n1]
+
+    def load_chain(self, net, k):
+        """Copy chain k's parameters into `net` (same architecture)."""
+        with torch.no_grad():
+            for p, o, n in zip(net.parameters(), self.offsets, self.numels):
+                p.copy_(self.theta2d[k, o:o + n].view(p.shape))
+
+    def use_grads(self, grads):
+        """Point the next launch at the vmapped gradients {name: [K, *shape]}
+        (None or a missing name: that tensor is frozen / has no gradient)."""
+        gl = [grads.get(nm) for nm in self.names]
+        if self.grad_mode == "flat":
+            for g, o, k in zip(gl, self.offsets, self.numels):
+                if g is not None:
+                    self.grad2d[:, o:o + k].copy_(g.reshape(self.K, k))
+            return
+        ptrs = []
+        for g, k in zip(gl, self.numels):
+            if g is None:
+                ptrs.append(0)
+                continue
+            if (g.dtype != torch.float32 or g.device != self.device or not g.is_contiguous()
+                    or g.numel() != self.K * k):
+                raise ValueError("StackedState: gradients must be contiguous fp32 [K, *shape]")
+            ptrs.append(g.data_ptr())
+        key = tuple(ptrs)
+        tab = self._tables.get(key)
+        if tab is None:
+            tab = self._build_table(ptrs)
+            if len(self._tables) >= 8:
+                self._tables.pop(next(iter(self._tables)))
+            self._tables[key] = tab
+        self.runs, self.nruns, self.gbase = tab
+
+    def _build_table(self, ptrs):
+        """One run per (chain, tensor) — a run must not span two gradient
+        tensors — plus a SKIP run over each chain's padding; chain k of tensor
+        i reads ptrs[i] + 4*(k*numel_i + j), i.e. base = that - 4*(flat index)."""
+        rows, bases = [], []
+        for k in range(self.K):
+            for o, n, a, ptr in zip(self.offsets, self.numels, self.attrs, ptrs):
+                start = k * self.stride + o
+                base = ptr + 4 * k * n - 4 * start if ptr else 0
+                at = a | (0 if ptr else L.ATTR_SKIP)
+                if ptr and base % 16:
+                    at |= L.ATTR_GUNALIGNED
+                rows.append((start + n, at))
+                bases.append(base)
+            if self.stride > self.n1:
+                rows.append(((k + 1) * self.stride, L.ATTR_SKIP))
+                bases.append(0)
+        nt = len(rows)
+        host = torch.empty(3 * nt, dtype=torch.int64).pin_memory()
+        h = host.numpy()
+        h[:2 * nt] = np.asarray(rows, dtype=np.int64).reshape(-1)
+        h[2 * nt:] = np.asarray(bases, dtype=np.int64)
+        dev = host.to(self.device, non_blocking=True)
+        return dev[:2 * nt].view(nt, 2), nt, dev[2 * nt:]
+
+    def diverged(self, reset=True):
+        bad = bool(self.nonfinite.item())
+        if bad and reset:
+            self.nonfinite.zero_()
+        return bad
+
+
+class StackedCSGHMC:
+    """K cyclical-SGHMC chains of `net` on one device, stepped together.
+
+    `args` carries the csghmc Runner's fields (lr, lr_head, epochs,
+    num_cycles, proportion_exploration, ND, hparams with prior_sig,
+    momentum_decay, Ninflate, nd, thin, nst, bias; device).  Chains are
+    keyed chain0 + k (default: rank * K, so chains stay distinct across
+    processes) with Philox seed `seed`."""
+
+    def __init__(self, net, K_, args, *, chain0=None, seed=None, init="copy", criterion=None,
+                 per_chain_batches=False, logger=None):
+        from . import chains
+        self.args, self.logger = args, logger
+        hp = args.hparams
+        self.net = net.to(args.device)
+        self.prior_sig = float(hp["prior_sig"])
+        self.momentum_decay = float(hp["momentum_decay"])
+        self.Ninflate, self.nd = float(hp["Ninflate"]), float(hp["nd"])
+        self.thin, self.nst = int(hp["thin"]), int(hp["nst"])
+        self.seed = int(getattr(args, "seed", 0) or 0) if seed is None else int(seed)
+        self.chain0 = chains.rank() * K_ if chain0 is None else int(chain0)
+        self.state = StackedState(self.net, K_, bias=str(hp["bias"]), init=init, seed=self.seed)
+        self.K = K_
+        self.criterion = criterion or torch.nn.CrossEntropyLoss()
+        self.sched = CyclicalSGMCMC(base_lr=args.lr, nbr_of_cycles=getattr(args, "num_cycles", 10),
+                                    epochs=args.epochs,
+                                    proportion_exploration=getattr(args, "proportion_exploration",
+                                                                   0.5))
+        self.step_count = 0
+        self.samples_per_cycle, self.mom1, self.mom2 = {}, {}, {}
+        self.draws = 0
+        st = self.state
+        self.trainable = [nm for nm, rg in zip(st.names, st.requires_grad) if rg]
+        self.buffers = dict(self.net.named_buffers())
+        xdim = 0 if per_chain_batches else None
+
+        def loss_fn(tp, fp, x, y):
+            out = functional_call(self.net, ({**tp, **fp}, self.buffers), (x,))
+            return self.criterion(out, y), out
+
+        self._grad = vmap(grad_and_value(loss_fn, has_aux=True),
+                          in_dims=(0, 0, xdim, xdim), randomness="different")
+        self._fwd = vmap(lambda p, x: functional_call(self.net, (p, self.buffers), (x,)),
+                         in_dims=(0, xdim), randomness="different")
+
+    def _split(self):
+        p = self.state.params
+        return ({nm: p[nm] for nm in self.trainable},
+                {nm: p[nm] for nm in p if nm not in self.trainable})
+
+    # ----------------------------------------------------------------- step
+    def gradients(self, x, y):
+        """Vmapped forward/backward of all chains: ({name: [K, *shape]},
+        loss [K], logits [K, B, C])."""
+        tp, fp = self._split()
+        grads, (loss, out) = self._grad(tp, fp, x, y)
+        return grads, loss.detach(), out.detach()
+
+    def step(self, x, y, lr, should_sample=False, collect=None):
+        """One cSGHMC step of all K chains (methods/csghmc.py:673-780 per chain):
+        vmapped forward/backward, then one fused launch.  Returns per-chain
+        (loss [K], logits [K, B, C]) on the device, without a host sync."""
+        grads, loss, out = self.gradients(x, y)
+        self.update(grads, lr, should_sample, collect)
+        return loss, out
+
+    def update(self, grads, lr, should_sample=False, collect=None):
+        """The fused launch over all chains for given gradients (step's second
+        half): v <- v(1-a) - lr(g + prior_sig theta) [+ noise]; theta += v;
+        Welford collect on sample steps."""
+        args, st = self.args, self.state
+        st.use_grads(grads)
+        lrs = (lr, lr * (args.lr_head / args.lr))
+        N = args.ND * self.Ninflate
+        ns = [self.nd * np.sqrt(2 * self.momentum_decay * v) / N for v in lrs]
+        ckind, m1, m2, ca = (L.COLLECT_NONE, None, None, 1.0) if collect is None else collect
+        K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=ns,
+                      noise_mode=L.NOISE_PHILOX if should_sample else L.NOISE_NONE,
+                      one_minus_alpha=1 - self.momentum_decay, prior_sig=self.prior_sig,
+                      collect=ckind, mom1=m1, mom2=m2, collect_a=ca, seed=self.seed,
+                      chain=self.chain0, step=self.step_count)
+        self.step_count += 1
+
+    def _collect_spec(self, c):
+        """Welford bookkeeping of methods/csghmc.py:333-348 (quirk Q2 double
+        count), shared by all chains (they sample on the same steps)."""
+        st = self.state
+        if c not in self.mom1:
+            self.mom1[c] = torch.zeros(st.n, dtype=torch.float32, device=st.device)
+            self.mom2[c] = torch.zeros(st.n, dtype=torch.float32, device=st.device)
+            return (L.COLLECT_WELFORD_INIT, self.mom1[c], self.mom2[c], 1.0), 1
+        n = self.samples_per_cycle.get(c, 0) + 1
+        return (L.COLLECT_WELFORD, self.mom1[c], self.mom2[c], float(n)), n
+
+    def train_one_epoch(self, loader, epoch):
+        """All batches of one epoch under the cyclical schedule
+        (methods/csghmc.py:246-384).  Returns per-chain (loss, error) arrays;
+        one host sync per epoch."""
+        dev, sched = self.args.device, self.sched
+        sched.current_epoch = epoch
+        bpe = len(loader)
+        loss_sum = torch.zeros(self.K, dtype=torch.float64, device=dev)
+        err_sum = torch.zeros(self.K, dtype=torch.int64, device=dev)
+        nb = 0
+        for b, (x, y) in enumerate(loader):
+            x, y = x.to(dev, non_blocking=True), y.to(dev, non_blocking=True)
+            lr = sched.calculate_lr(epoch=epoch, batch=b, batches_per_epoch=bpe)
+            ss = sched.should_sample(epoch=epoch, batch=b, batches_per_epoch=bpe) \
+                and b % self.thin == 0
+            collect, cnt, c = None, None, None
+            if ss:
+                c = sched.get_cycle_number(epoch=epoch, batch=b, batches_per_epoch=bpe)
+                collect, cnt = self._collect_spec(c)
+            loss, out = self.step(x, y, lr, should_sample=ss, collect=collect)
+            if ss:  # Q2: the reference bumps the count twice per sample
+                self.samples_per_cycle[c] = cnt + 1
+            bs = y.shape[-1]
+            loss_sum += loss.double() * bs
+            err_sum += out.argmax(-1).ne(y).sum(-1)
+            nb += bs
+        return (loss_sum / nb).cpu().numpy(), (err_sum.double() / nb).cpu().numpy()
+
+    # ----------------------------------------------------------- predictive
+    def chain_logits(self, x):
+        """[K, B, C] logits of every chain at its current theta."""
+        with torch.no_grad():
+            return self._fwd(self.state.params, x)
+
+    def _draw_params(self, c, out):
+        """Fill `out` ([K*stride]) with one posterior draw of every chain from
+        cycle c's Welford moments (methods/csghmc.py:446-468; var = M2/(n-1),
+        1e-12 for a single sample), chain k keyed chain0 + k."""
+        st = self.state
+        n = self.samples_per_cycle.get(c, 0)
+        if n > 1:
+            m2, vm, ratio = self.mom2[c], L.VAR_WELFORD, float(n - 1)
+        else:
+            m2, vm, ratio = None, L.VAR_GIVEN, 1.0
+        K.posterior_sample(out, self.mom1[c], m2, var_mode=vm, ratio=ratio, seed=self.seed,
+                           chain=self.chain0, step=EVAL_STEP_BASE + self.draws,
+                           chain_groups=st.chain_groups)
+        self.draws += 1
+
+    def predictive_logprob(self, x):
+        """log of the predictive probability averaged uniformly over the K
+        chains x (nst draws of) every collected cycle; the chains' current
+        theta while no cycle has been collected."""
+        st = self.state
+        with torch.no_grad():
+            if not self.mom1:
+                lp = F.log_softmax(self.chain_logits(x), dim=-1)
+                return lp.logsumexp(0) - math.log(self.K)
+            buf = torch.empty_like(st.theta)
+            views = {nm: buf.view(self.K, st.stride)[:, o:o + k].view(self.K, *s)
+                     for nm, o, k, s in zip(st.names, st.offsets, st.numels, st.shapes)}
+            comps = []
+            for c in sorted(self.mom1):
+                for _ in range(max(1, self.nst)):
+                    if self.nst == 0:
+                        buf.copy_(self.mom1[c])
+                    else:
+                        self._draw_params(c, buf)
+                    comps.append(F.log_softmax(self._fwd(views, x), dim=-1))
+            lp = torch.cat(comps, 0)  # [K * draws, B, C]
+            return lp.logsumexp(0) - math.log(lp.shape[0])
+
+    def evaluate(self, loader):
+        """(NLL, error) of the stacked predictive over a data loader."""
+        dev = self.args.device
+        loss, err, nb = 0.0, 0, 0
+        for x, y in loader:
+            x, y = x.to(dev), y.to(dev)
+            lp = self.predictive_logprob(x)
+            loss += F.nll_loss(lp, y, reduction="sum").item()
+            err += lp.argmax(-1).ne(y).sum().item()
+            nb += len(y)
+        return loss / nb, err / nb
+
+    def train(self, train_loader, test_loader=None):
+        """Run args.epochs epochs; logs per-chain losses and, after every
+        epoch that ends a cycle, the stacked predictive on test_loader."""
+        log = self.logger.info if self.logger is not None else (lambda *_: None)
+        hist = []
+        for ep in range(self.args.epochs):
+            tic = time.time()
+            lt, et = self.train_one_epoch(train_loader, ep)
+            if self.state.diverged():
+                log(f"[Epoch {ep}] a chain wrote a non-finite theta")
+            rec = {"epoch": ep, "loss": lt.tolist(), "error": et.tolist(),
+                   "seconds": time.time() - tic}
+            log(f"[Epoch {ep}/{self.args.epochs}] {self.K} chains: loss = {lt.mean():.4f} "
+                f"(min {lt.min():.4f}, max {lt.max():.4f}), error = {et.mean():.4f} "
+                f"({rec['seconds']:.2f} s)")
+            if test_loader is not None and self.sched.last_in_cycle(
+                    epoch=ep, batch=len(train_loader) - 1, batches_per_epoch=len(train_loader)):
+                rec["test"] = self.evaluate(test_loader)
+                log(f"(Epoch {ep}) stacked predictive: loss = {rec['test'][0]:.4f}, "
+                    f"error = {rec['test'][1]:.4f}")
+            hist.append(rec)
+        return hist

@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define BDL_ABI_VERSION 5
+#define BDL_ABI_VERSION 6
 
 typedef enum bdl_status {
   BDL_OK = 0,
@@ -189,6 +189,16 @@ typedef struct bdl_step_args {
    * pointers and the run table shifted to it) draws exactly the noise the
    * whole-vector launch draws there.  0 for whole-vector launches. */
   uint64_t philox_offset;
+  /* Stacked chains (0: the vectors hold one chain).  > 0: they hold
+   * consecutive chains of 4*chain_groups elements each — chain k's element j
+   * at 4*chain_groups*k + j, the tail of each chain's slot beyond its own n
+   * covered by a BDL_ATTR_SKIP run — and chain k draws its Philox noise keyed
+   * chain + k with the element index inside its slot: exactly the noise of a
+   * one-chain launch with chain id chain + k.  The run table spans all chains
+   * (one run per chain and tensor in grad_base mode).  Requires n/4 +
+   * philox_offset < 2^32.  Replaces running K reference processes, one chain
+   * each, on one device. */
+  uint64_t chain_groups;
 } bdl_step_args;
 
 /* Extra state and scalars of the Adam-preconditioned SGHMC step.  Per element,
@@ -257,6 +267,7 @@ typedef struct bdl_sample_args {
   float inv_ratio;         /* WELFORD: nonzero -> multiply by it (torch-on-GPU rounding) */
   float pad;
   uint64_t seed, chain, step;
+  uint64_t chain_groups;   /* stacked chains, as bdl_step_args.chain_groups (0: one) */
 } bdl_sample_args;
 
 int bdl_version(void);

@@ -167,6 +167,16 @@ def test_entry_points_validate_before_touching_the_device():
     a.grad_base, a.nruns = 0x5000, 2731
     assert h.bdl_sgmcmc_step(a, None) == -5                         # runs + bases > 64 KiB LDS
     a.grad, a.grad_base, a.nruns = 0x2000, None, 1
+    # stacked chains: every float4 group index (+ philox_offset) below 2^32
+    a.chain_groups, a.n = 1 << 32, 8
+    assert h.bdl_sgmcmc_step(a, None) == -3                         # chain_groups >= 2^32
+    a.chain_groups, a.n, a.philox_offset = 2, 8, (1 << 32) - 1
+    assert h.bdl_sgmcmc_step(a, None) == -3                         # offset + n/4 >= 2^32
+    assert b"stacked chains" in h.bdl_last_error()
+    sa = L.SampleArgs()
+    sa.n, sa.out, sa.mom1, sa.noise_mode, sa.chain_groups = 8, 0x1000, 0x2000, L.NOISE_PHILOX, 1 << 32
+    assert h.bdl_posterior_sample(sa, None) == -3
+    a.chain_groups, a.philox_offset = 0, 0
     a.method = L.SGLD
     assert h.bdl_sgmcmc_step(a, None) == -1                         # sgld needs prior_mean
     a.n = 0
