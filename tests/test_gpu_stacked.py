@@ -171,6 +171,26 @@ def test_stacked_training_learns_and_evaluates():
     assert not S.state.diverged()
 
 
+def test_stacked_graph_replay_is_bit_identical_to_eager():
+    """HIP-graph replay of the vmapped forward/backward: same chains, same
+    batches, same theta / momentum bit for bit after mixed steps."""
+    from bayesdll_amd import stacked
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(4)
+        S = stacked.StackedCSGHMC(Net().cuda(), 5, _args(), init="reinit", seed=2, graph=graph)
+        g = torch.Generator().manual_seed(9)
+        for k in range(6):
+            x = torch.randn(24, 13, generator=g).cuda()
+            y = torch.randint(0, 5, (24,), generator=g).cuda()
+            loss, out = S.step(x, y, 0.05 / (k + 1), should_sample=k % 2 == 1)
+        torch.cuda.synchronize()
+        runs.append((S.state.theta.clone(), S.state.mom.clone(), loss.clone(), len(S._graphs)))
+    assert runs[0][3] == 0 and runs[1][3] == 1
+    for a, b in zip(runs[0][:3], runs[1][:3]):
+        assert torch.equal(a, b)
+
+
 def test_stacked_refuses_batchnorm_statistics():
     from bayesdll_amd import stacked
     net = nn.Sequential(nn.Linear(4, 4), nn.BatchNorm1d(4)).cuda()

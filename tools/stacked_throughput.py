@@ -4,7 +4,7 @@ vs one chain per step (the fused Runner Model, eager and HIP-graph).
 Synthetic MNIST-shaped batch, shared by the chains; every 10th step a noise
 (sample) step, as in e2e_compare.py.  Informational; not the bench metric.
 
-    BACKBONE=mlp_mnist BATCH=128 STEPS=50 KS=1,4,16,64 python tools/stacked_throughput.py
+    BACKBONE=mlp_mnist BATCH=128 STEPS=50 KS=1,4,16,64,256 python tools/stacked_throughput.py
 """
 import os
 import sys
@@ -23,7 +23,7 @@ def main():
     name = os.environ.get("BACKBONE", "mlp_mnist")
     batch = int(os.environ.get("BATCH", "128"))
     steps = int(os.environ.get("STEPS", "50"))
-    ks = [int(k) for k in os.environ.get("KS", "1,4,16,64").split(",")]
+    ks = [int(k) for k in os.environ.get("KS", "1,4,16,64,256").split(",")]
     dev = "cuda"
     x = torch.randn(batch, 1, 28, 28, device=dev)
     y = torch.randint(0, 10, (batch,), device=dev)
@@ -53,9 +53,10 @@ def main():
                            proportion_exploration=0.5, ND=60000, device=dev, seed=0,
                            hparams={"prior_sig": 1.0, "momentum_decay": 0.1, "Ninflate": 1.0,
                                     "nd": 1.0, "thin": 1, "nst": 0, "bias": "informative"})
-    for K_ in ks:
+    for K_, graph in [(k, g) for k in ks for g in (False, True)]:
         torch.manual_seed(0)
-        S = stacked.StackedCSGHMC(backbone(name, 10).to(dev), K_, args, init="reinit")
+        S = stacked.StackedCSGHMC(backbone(name, 10).to(dev), K_, args, init="reinit",
+                                  graph=graph)
         ms = timed(lambda k: S.step(x, y, 1e-4, should_sample=k % 10 == 0))
         # the fused update alone, over K * n elements (20 B/element, explore)
         grads, _, _ = S.gradients(x, y)
@@ -69,7 +70,8 @@ def main():
         torch.cuda.synchronize()
         ums = e0.elapsed_time(e1) / 20
         gbs = 20 * S.state.n / (ums * 1e-3) / 1e9
-        print(f"{name} batch {batch}: {K_} stacked chains ({S.state.grad_mode} grads, "
+        print(f"{name} batch {batch}: {K_} stacked chains{' + graph' if graph else ''} "
+              f"({S.state.grad_mode} grads, "
               f"{S.state.nruns} runs): {ms:.3f} ms/step, {K_ * 1e3 / ms:.0f} chain-steps/s; "
               f"update {ums:.4f} ms ({gbs:.0f} GB/s over {S.state.n} elements)", flush=True)
         del S, grads
