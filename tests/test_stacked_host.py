@@ -1,0 +1,137 @@
+"""Host logic of bayesdll_amd.stacked on the CPU (no launches): the stacked
+layout, the per-(chain, tensor) run / gradient-base table, the flat fallback,
+and the vmapped gradients against per-chain autograd.  The launches themselves
+are tested on the GPU (tests/test_gpu_stacked.py)."""
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+
+class Net(nn.Module):
+    readout_name = "head"
+
+    def __init__(self):
+        super().__init__()
+        self.body = nn.Linear(13, 7)   # 91 + 7
+        self.head = nn.Linear(7, 5)    # 35 + 5  -> n = 138, stride 140
+
+    def forward(self, x):
+        return self.head(torch.tanh(self.body(x)))
+
+
+def _args():
+    return SimpleNamespace(lr=5e-2, lr_head=1e-1, epochs=2, num_cycles=2,
+                           proportion_exploration=0.5, ND=64, device="cpu", seed=7,
+                           hparams={"prior_sig": 1.0, "momentum_decay": 0.1, "Ninflate": 1.0,
+                                    "nd": 1.0, "thin": 1, "nst": 0, "bias": "informative"})
+
+
+@pytest.fixture
+def host_only(monkeypatch):
+    """Let the state live on the CPU and record launches instead of making them."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    calls = []
+    monkeypatch.setattr(L, "require_hip", lambda *a, **k: None)
+    monkeypatch.setattr(torch.Tensor, "pin_memory", lambda self: self)
+    monkeypatch.setattr(K, "sgmcmc_step", lambda st, m, **kw: calls.append((st, m, kw)))
+    return calls
+
+
+def test_stacked_layout_and_grad_table(host_only):
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import stacked
+    torch.manual_seed(0)
+    S = stacked.StackedCSGHMC(Net(), 3, _args(), chain0=4, init="reinit", seed=1)
+    st = S.state
+    assert (st.n1, st.stride, st.n, st.chain_groups) == (138, 140, 420, 35)
+    # chains start from different re-initialisations; padding is zero
+    assert not torch.equal(st.theta2d[0], st.theta2d[1])
+    assert torch.count_nonzero(st.theta2d[:, 138:]) == 0
+    # parameter views alias the stacked theta
+    assert st.params["head.bias"].data_ptr() == st.theta2d.data_ptr() + 4 * (91 + 7 + 35)
+    x, y = torch.randn(16, 13), torch.randint(0, 5, (16,))
+    grads, loss, out = S.gradients(x, y)
+    assert loss.shape == (3,) and out.shape == (3, 16, 5)
+    S.update(grads, 0.05, should_sample=True)
+    (sst, method, kw), = host_only
+    assert method == L.CSGHMC and kw["chain"] == 4 and kw["noise_mode"] == L.NOISE_PHILOX
+    runs = st.runs.numpy()
+    assert st.nruns == 3 * 5 and runs.shape == (15, 2)
+    ends = runs[:, 0].tolist()
+    assert ends == [91, 98, 133, 138, 140, 231, 238, 273, 278, 280, 371, 378, 413, 418, 420]
+    attrs = runs[:, 1] & 0x7
+    assert attrs.tolist() == [2, 2, 3, 3, 4] * 3          # PRIOR, +HEAD, SKIP padding
+    bases = st.gbase.numpy()
+    names = st.names
+    for k in range(3):
+        for i, nm in enumerate(names):
+            r = 5 * k + i
+            start = k * 140 + st.offsets[i]
+            want = grads[nm].data_ptr() + 4 * k * st.numels[i] - 4 * start
+            assert bases[r] == want
+            assert bool(runs[r, 1] & L.ATTR_GUNALIGNED) == bool(want % 16)
+        assert bases[5 * k + 4] == 0
+    # same gradient tensors again -> the cached table
+    S.update(grads, 0.05)
+    assert host_only[-1][0].runs is sst.runs
+
+
+def test_stacked_flat_fallback_copies_gradients(host_only, monkeypatch):
+    from bayesdll_amd import stacked
+    monkeypatch.setattr(stacked, "MAX_TENSOR_RUNS", 4)
+    S = stacked.StackedCSGHMC(Net(), 2, _args())
+    st = S.state
+    assert st.grad_mode == "flat" and st.gbase is None
+    grads, _, _ = S.gradients(torch.randn(8, 13), torch.randint(0, 5, (8,)))
+    S.update(grads, 0.01)
+    for k in range(2):
+        for nm, o, n in zip(st.names, st.offsets, st.numels):
+            assert torch.equal(st.grad2d[k, o:o + n], grads[nm][k].reshape(-1))
+    # merged runs per chain; padding skipped
+    ends = st.runs[:, 0].tolist()
+    assert ends[-1] == 280 and 140 in ends and 138 in ends
+
+
+def test_stacked_gradients_equal_per_chain_autograd_on_cpu(host_only):
+    from bayesdll_amd import stacked
+    torch.manual_seed(2)
+    S = stacked.StackedCSGHMC(Net(), 4, _args(), init="reinit", seed=3)
+    x, y = torch.randn(32, 13), torch.randint(0, 5, (32,))
+    grads, loss, _ = S.gradients(x, y)
+    net = Net()
+    for k in range(4):
+        S.state.load_chain(net, k)
+        net.zero_grad()
+        lk = nn.CrossEntropyLoss()(net(x), y)
+        lk.backward()
+        assert abs(lk.item() - loss[k].item()) < 1e-5
+        for nm, p in net.named_parameters():
+            np.testing.assert_allclose(grads[nm][k].numpy(), p.grad.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_stacked_frozen_parameter_is_skipped(host_only):
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import stacked
+    net = Net()
+    net.body.bias.requires_grad_(False)
+    S = stacked.StackedCSGHMC(net, 2, _args())
+    grads, _, _ = S.gradients(torch.randn(8, 13), torch.randint(0, 5, (8,)))
+    assert "body.bias" not in grads
+    S.update(grads, 0.01)
+    runs = S.state.runs.numpy()
+    assert runs[1, 1] & L.ATTR_SKIP and runs[6, 1] & L.ATTR_SKIP
+    assert S.state.gbase.numpy()[1] == 0
+
+
+def test_stacked_refuses_what_it_cannot_stack(host_only):
+    from bayesdll_amd import stacked
+    with pytest.raises(ValueError, match="BatchNorm"):
+        stacked.StackedState(nn.Sequential(nn.Linear(4, 4), nn.BatchNorm1d(4)), 2)
+    with pytest.raises(ValueError, match="K must be"):
+        stacked.StackedState(Net(), 0)
+    with pytest.raises(ValueError, match="init"):
+        stacked.StackedState(Net(), 2, init="zeros")
