@@ -105,6 +105,9 @@ def build_parser():
                     help="overlap the fused update with backward, bucket by bucket (cSGHMC)")
     ap.add_argument("--resume_state", action="store_true",
                     help="checkpoints carry what an exact resume needs")
+    ap.add_argument("--stacked_chains", type=int, default=0,
+                    help="csghmc only: K > 0 chains per device stepped together "
+                         "(bayesdll_amd.stacked; no BatchNorm statistics)")
     return ap
 
 
@@ -196,6 +199,15 @@ def main(argv=None):
         net0 = net0.to(device)
     net = net.to(device)
 
+    if args.stacked_chains > 0:
+        if args.method != "csghmc":
+            raise ValueError("--stacked_chains: csghmc only")
+        from .stacked import StackedCSGHMC
+        S = StackedCSGHMC(net, args.stacked_chains, args, logger=logger, init="reinit",
+                          graph=args.graph)
+        logger.info(f"{args.stacked_chains} stacked chains on this device "
+                    f"(chain ids {S.chain0}..{S.chain0 + S.K - 1})")
+        return S.train(train_loader, test_loader)
     runner_cls = importlib.import_module(f"bayesdll_amd.{args.method}").Runner
     runner = runner_cls(net, net0, args, logger)
     return runner.train(train_loader, val_loader, test_loader)

@@ -53,6 +53,25 @@ def test_cli_end_to_end_tiny(method, tmp_path):
 
 
 @pytest.mark.gpu
+def test_cli_stacked_chains(tmp_path):
+    """--stacked_chains K: K csghmc chains per device through the CLI (graph replay)."""
+    import numpy as np
+    from bayesdll_amd.run import main
+    hp = ("prior_sig=1.0,Ninflate=1.0,nd=0.01,burnin=0,momentum_decay=0.18,thin=1,"
+          "bias=informative,nst=2")
+    hist = main(["--method", "csghmc", "--dataset", "mnist", "--backbone", "mlp_mnist",
+                 "--epochs", "2", "--num_cycles", "2", "--batch_size", "64", "--lr", "1e-2",
+                 "--train_size", "256", "--test_size", "64", "--val_heldout", "0",
+                 "--stacked_chains", "4", "--graph", "--hparams", hp,
+                 "--log_dir", str(tmp_path)])
+    assert len(hist) == 2 and all(len(h["loss"]) == 4 for h in hist)
+    assert all(np.isfinite(h["loss"]).all() for h in hist)
+    assert all("test" in h and np.isfinite(h["test"][0]) for h in hist)
+    text = next(tmp_path.rglob("logs.txt")).read_text()
+    assert "4 stacked chains" in text
+
+
+@pytest.mark.gpu
 def test_cli_vit_l_32_csghmc_config4(tmp_path):
     """Config 4 at the Runner level: ViT-L/32 (306.5 M parameters) cSGHMC
     through the CLI on Pets-shaped synthetic data — cyclical schedule, Welford
