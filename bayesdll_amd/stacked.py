@@ -227,7 +227,9 @@ class StackedCSGHMC:
         self.thin, self.nst = int(hp["thin"]), int(hp["nst"])
         self.seed = int(getattr(args, "seed", 0) or 0) if seed is None else int(seed)
         self.chain0 = chains.rank() * K_ if chain0 is None else int(chain0)
-        self.state = StackedState(self.net, K_, bias=str(hp["bias"]), init=init, seed=self.seed)
+        # re-initialisation seeds seed + chain id: distinct across processes too
+        self.state = StackedState(self.net, K_, bias=str(hp["bias"]), init=init,
+                                  seed=self.seed + self.chain0)
         self.K = K_
         self.criterion = criterion or torch.nn.CrossEntropyLoss()
         self.sched = CyclicalSGMCMC(base_lr=args.lr, nbr_of_cycles=getattr(args, "num_cycles", 10),
@@ -381,7 +383,14 @@ class StackedCSGHMC:
     def predictive_logprob(self, x):
         """log of the predictive probability averaged uniformly over the K
         chains x (nst draws of) every collected cycle; the chains' current
-        theta while no cycle has been collected."""
+        theta while no cycle has been collected.  With one process per GPU
+        (torch.distributed initialised) the processes' stacked predictives are
+        averaged too (chains.average_predictive: one all-reduce)."""
+        from . import chains
+        lp = self._local_logprob(x)
+        return chains.average_predictive(lp) if chains.world() > 1 else lp
+
+    def _local_logprob(self, x):
         st = self.state
         with torch.no_grad():
             if not self.mom1:

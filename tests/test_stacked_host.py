@@ -2,6 +2,8 @@
 layout, the per-(chain, tensor) run / gradient-base table, the flat fallback,
 and the vmapped gradients against per-chain autograd.  The launches themselves
 are tested on the GPU (tests/test_gpu_stacked.py)."""
+import os
+import socket
 from types import SimpleNamespace
 
 import numpy as np
@@ -135,3 +137,47 @@ def test_stacked_refuses_what_it_cannot_stack(host_only):
         stacked.StackedState(Net(), 0)
     with pytest.raises(ValueError, match="init"):
         stacked.StackedState(Net(), 2, init="zeros")
+
+
+def _stacked_worker(r, world, port, q):
+    import torch.distributed as dist
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import stacked
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    L.require_hip = lambda *a, **k: None
+    dist.init_process_group("gloo", rank=r, world_size=world)
+    try:
+        torch.manual_seed(0)
+        S = stacked.StackedCSGHMC(Net(), 2, _args(), init="reinit", seed=10 + 2 * r)
+        x = torch.randn(6, 13, generator=torch.Generator().manual_seed(5))
+        q.put((r, S.chain0, S.chain_logits(x), S.predictive_logprob(x)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_stacked_predictive_averages_over_processes():
+    """Two processes x two stacked chains (gloo): chain ids rank*K + k, and
+    every process returns the predictive averaged over all four chains."""
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_stacked_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, c0, logits, lp = q.get(timeout=120)
+        res[r] = (c0, logits, lp)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] == 0 and res[1][0] == 2
+    probs = torch.cat([res[r][1] for r in range(2)]).softmax(-1)  # [4, B, C]
+    want = probs.mean(0).log()
+    for r in range(2):
+        torch.testing.assert_close(res[r][2], want, rtol=1e-5, atol=1e-6)
