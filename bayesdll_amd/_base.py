@@ -67,6 +67,15 @@ class FusedModelBase(nn.Module):
     tune_method = "sgld"  # which production kernel autotune_once times for this sampler
     extra_vectors = ()    # further per-element state placed with the chain (FlatState.extra)
 
+    # set by the bundled Runners: Model.forward returns the loss as a device
+    # scalar instead of loss.item(), so a step issues no host synchronisation
+    defer_loss = False
+
+    def _result(self, loss, out):
+        """(loss.item(), logits) as the reference's Model.forward returns them,
+        or (detached device loss, logits) under defer_loss."""
+        return (loss.detach() if self.defer_loss else loss.item()), out.detach()
+
     def __init__(self):
         super().__init__()
         self.noise_mode = default_noise_mode()

@@ -64,6 +64,19 @@ class PosteriorDraw:
         self.count += 1
 
 
+def defer_loss(runner):
+    """Let the Runner's Model return device losses (no per-step host sync);
+    BDL_SYNC_LOSS=1 restores the reference's per-step loss.item()."""
+    runner.model.defer_loss = os.environ.get("BDL_SYNC_LOSS", "0") != "1"
+
+
+def add_loss(acc, loss_, n):
+    """acc + loss_ * n, the reference's float64 running sum (`loss += loss_ *
+    len(y)`), kept on the device when loss_ is a device scalar: the same
+    float64 operations in the same order, so float(acc) is the same number."""
+    return acc + (loss_.double() if torch.is_tensor(loss_) else loss_) * n
+
+
 def chain_world():
     return chains.world()
 

@@ -179,4 +179,4 @@ class Model(FusedModelBase):
             if mom:
                 sgd.has_buffer = True
         self.step_count += 1
-        return loss.item(), out.detach()
+        return self._result(loss, out)

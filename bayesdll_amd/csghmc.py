@@ -161,6 +161,7 @@ class Runner:
 
     def train_one_epoch(self, train_loader):
         """methods/csghmc.py:246-384 with the update + Welford fused on device."""
+        R.defer_loss(self)
         args, logger = self.args, self.logger
         self.net.train()
         loss, error, nb_samples = 0, 0, 0
@@ -194,7 +195,7 @@ class Runner:
 
             pred = out.data.max(dim=1)[1]
             err = pred.ne(y.data).sum()
-            loss += loss_ * len(y)
+            loss = R.add_loss(loss, loss_, len(y))
             errs.append(err)  # summed once per epoch: no second host sync per step
             nb_samples += len(y)
 
@@ -223,7 +224,7 @@ class Runner:
                         self.save_ckpt(epoch=sched.current_epoch)
                     self._cycle_completed(cycle_number)
         error = int(torch.stack(errs).sum().item()) if errs else 0
-        return loss / nb_samples, error / nb_samples, cycle_updated
+        return float(loss) / nb_samples, error / nb_samples, cycle_updated
 
     def _cycle_completed(self, cycle_number):
         """Hook after a newly completed cycle was scored and checkpointed."""
@@ -357,7 +358,7 @@ class Model(FusedModelBase):
                     sub, L.CSGHMC, noise_mode=nm, mom1=sl(m1, start, start + sub.n),
                     mom2=sl(m2, start, start + sub.n), philox_offset=start // 4, **kw))
             self.step_count += 1
-            return loss.item(), out.detach()
+            return self._result(loss, out)
         loss, out = self.forward_backward(st, net, x, y, criterion)
         # the reference draws randn_like on every step, even when the noise is
         # dropped (:766): the torch/external sources are advanced every step
@@ -365,4 +366,4 @@ class Model(FusedModelBase):
         K.sgmcmc_step(st, L.CSGHMC, noise_mode=nmode if should_sample else L.NOISE_NONE,
                       mom1=m1, mom2=m2, **kw)
         self.step_count += 1
-        return loss.item(), out.detach()
+        return self._result(loss, out)

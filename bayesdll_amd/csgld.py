@@ -140,6 +140,7 @@ class Runner:
 
     def train_one_epoch(self, train_loader):
         """methods/csgld.py:195-331, with Model + clip + SGD + moments fused."""
+        R.defer_loss(self)
         args, logger = self.args, self.logger
         self.net.train()
         loss, error, nb = 0, 0, 0
@@ -179,7 +180,7 @@ class Runner:
                                     clip_grad=clip)
             pred = out.data.max(dim=1)[1]
             err = pred.ne(y.data).sum()
-            loss += loss_ * len(y)
+            loss = R.add_loss(loss, loss_, len(y))
             errs.append(err)  # summed once per epoch: no second host sync per step
             nb += len(y)
 
@@ -204,7 +205,7 @@ class Runner:
                         self.save_ckpt(epoch=sched.current_epoch)
                     self._cycle_completed(cycle_number)
         error = int(torch.stack(errs).sum().item()) if errs else 0
-        return loss / nb, error / nb, cycle_updated
+        return float(loss) / nb, error / nb, cycle_updated
 
     def _variance_source(self, cycle):
         """methods/csgld.py:394-400: ratio*(m2 - m1^2) (ratio = spc/(spc-1)

@@ -78,4 +78,4 @@ class Model(FusedModelBase):
             K.sgmcmc_step(st, L.SGHMC, **common, collect=ckind, mom1=m1, mom2=m2, collect_a=ca,
                           collect_b=cb)
         self.step_count += 1
-        return loss.item(), out.detach()
+        return self._result(loss, out)

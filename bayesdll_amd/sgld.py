@@ -172,6 +172,7 @@ class Runner:
 
     def train_one_epoch(self, train_loader, collect, bi):
         """methods/sgld.py:193-250 with Model + SGD step + moments fused."""
+        R.defer_loss(self)
         args, logger = self.args, self.logger
         self.net.train()
         loss, error, nb = 0, 0, 0
@@ -189,7 +190,7 @@ class Runner:
                                     self.Ninflate, self.nd, sgd=self.sgd, collect=spec)
             pred = out.data.max(dim=1)[1]
             err = pred.ne(y.data).sum()
-            loss += loss_ * len(y)
+            loss = R.add_loss(loss, loss_, len(y))
             errs.append(err)  # summed once per epoch: no second host sync per step
             nb += len(y)
             bi += 1
@@ -197,7 +198,7 @@ class Runner:
                 logger.info("(post-burnin) accumulate posterior samples")
                 self.post_theta_cnt += 1
         error = int(torch.stack(errs).sum().item()) if errs else 0
-        return loss / nb, error / nb, bi
+        return float(loss) / nb, error / nb, bi
 
     # --------------------------------------------------------------- evaluate
     def get_var_source(self):
@@ -323,4 +324,4 @@ class Model(FusedModelBase):
             if mom:
                 sgd.has_buffer = True
         self.step_count += 1
-        return loss.item(), out.detach()
+        return self._result(loss, out)
