@@ -250,8 +250,9 @@ class StackedCSGHMC:
 
         self._grad = vmap(grad_and_value(loss_fn, has_aux=True),
                           in_dims=(0, 0, xdim, xdim), randomness="different")
+        # evaluation: every chain sees the same batch
         self._fwd = vmap(lambda p, x: functional_call(self.net, (p, self.buffers), (x,)),
-                         in_dims=(0, xdim), randomness="different")
+                         in_dims=(0, None), randomness="different")
 
     def _split(self):
         p = self.state.params

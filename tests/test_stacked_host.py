@@ -115,6 +115,28 @@ def test_stacked_gradients_equal_per_chain_autograd_on_cpu(host_only):
             np.testing.assert_allclose(grads[nm][k].numpy(), p.grad.numpy(), rtol=1e-5, atol=1e-6)
 
 
+def test_stacked_per_chain_batches(host_only):
+    """per_chain_batches: chain k trains on batch k ([K, B, ...]) and is
+    evaluated on the shared batch."""
+    from bayesdll_amd import stacked
+    torch.manual_seed(4)
+    S = stacked.StackedCSGHMC(Net(), 3, _args(), init="reinit", seed=1, per_chain_batches=True)
+    x, y = torch.randn(3, 8, 13), torch.randint(0, 5, (3, 8))
+    grads, loss, out = S.gradients(x, y)
+    assert out.shape == (3, 8, 5)
+    net = Net()
+    for k in range(3):
+        S.state.load_chain(net, k)
+        net.zero_grad()
+        lk = nn.CrossEntropyLoss()(net(x[k]), y[k])
+        lk.backward()
+        assert abs(lk.item() - loss[k].item()) < 1e-5
+        np.testing.assert_allclose(grads["head.weight"][k].numpy(), net.head.weight.grad.numpy(),
+                                   rtol=1e-5, atol=1e-6)
+    assert S.chain_logits(x[0]).shape == (3, 8, 5)
+    assert S.predictive_logprob(x[0]).shape == (8, 5)
+
+
 def test_stacked_frozen_parameter_is_skipped(host_only):
     from bayesdll_amd import _lib as L
     from bayesdll_amd import stacked
