@@ -106,7 +106,7 @@ def build_parser():
     ap.add_argument("--resume_state", action="store_true",
                     help="checkpoints carry what an exact resume needs")
     ap.add_argument("--stacked_chains", type=int, default=0,
-                    help="csghmc only: K > 0 chains per device stepped together "
+                    help="csghmc / sgld: K > 0 chains per device stepped together "
                          "(bayesdll_amd.stacked; no BatchNorm statistics)")
     return ap
 
@@ -200,11 +200,12 @@ def main(argv=None):
     net = net.to(device)
 
     if args.stacked_chains > 0:
-        if args.method != "csghmc":
-            raise ValueError("--stacked_chains: csghmc only")
-        from .stacked import StackedCSGHMC
-        S = StackedCSGHMC(net, args.stacked_chains, args, logger=logger, init="reinit",
-                          graph=args.graph)
+        from . import stacked
+        cls = {"csghmc": stacked.StackedCSGHMC, "sgld": stacked.StackedSGLD}.get(args.method)
+        if cls is None:
+            raise ValueError("--stacked_chains: csghmc or sgld")
+        S = cls(net, args.stacked_chains, args, logger=logger, init="reinit", graph=args.graph,
+                net0=net0)
         logger.info(f"{args.stacked_chains} stacked chains on this device "
                     f"(chain ids {S.chain0}..{S.chain0 + S.K - 1})")
         return S.train(train_loader, test_loader)

@@ -1,4 +1,4 @@
-"""Stacked chains: K independent cSGHMC chains of one network on one device.
+"""Stacked chains: K independent cSGHMC (or SGLD) chains of one network on one device.
 
 The reference runs one chain per process (methods/csghmc.py:41); its own
 recipe for more chains is more processes.  On an MI355X a small network
@@ -22,10 +22,11 @@ update bit for bit given the same gradient (tests/test_gpu_stacked.py).  The
 gradients come from batched GEMMs, so a stacked chain agrees with a separately
 run chain to rounding, not bitwise.
 
-Scope: cSGHMC (the north-star sampler) with the reference's cyclical
-schedule, thinning and per-cycle Welford moments; the predictive averages
-probabilities uniformly over chains and (nst posterior draws of) collected
-cycles.  Networks with BatchNorm running statistics are refused (vmap cannot
+Scope: StackedCSGHMC (the north-star sampler: cyclical schedule, thinning,
+per-cycle Welford moments) and StackedSGLD (SGLD + SGD momentum, prior mean
+theta0, burn-in, thinned running moments); the predictive averages
+probabilities uniformly over chains and (nst posterior draws of) the collected
+components.  Networks with BatchNorm running statistics are refused (vmap cannot
 update shared buffers per chain), and every trainable parameter must take part
 in the forward pass (torch.func returns zeros, not None, for unused inputs).
 """
@@ -55,7 +56,7 @@ class StackedState:
     chain_groups, nonfinite) are what kernels._step_args reads."""
 
     def __init__(self, net, K_, *, readout_name=None, bias="informative", init="copy",
-                 seed=0, need_mom=True):
+                 seed=0, need_mom=True, need_prior=False, net0=None):
         import torch.nn as nn
         if K_ < 1:
             raise ValueError("StackedState: K must be >= 1")
@@ -106,7 +107,19 @@ class StackedState:
         self.theta = self.theta2d.view(-1)
         self.mom2d = torch.zeros(self.K, self.stride, **f32) if need_mom else None
         self.mom = None if self.mom2d is None else self.mom2d.view(-1)
-        self.prior, self.noise = None, None
+        self.noise = None
+        # prior mean theta0 (SGLD): net0's parameters (zeros without one) in
+        # every chain's slot
+        self.prior = None
+        if need_prior:
+            p2 = torch.zeros(self.K, self.stride, **f32)
+            if net0 is not None:
+                p0 = [q.detach().reshape(-1).float() for q in net0.parameters()]
+                if [q.numel() for q in p0] != self.numels:
+                    raise ValueError("StackedState: net0 does not match net's parameter shapes")
+                with torch.no_grad():
+                    p2[:, :self.n1].copy_(torch.cat(p0).to(dev))
+            self.prior = p2.view(-1)
         self.nonfinite = torch.zeros(1, dtype=torch.int32, device=dev)
         self.params = {nm: self.theta2d[:, o:o + k].view(self.K, *s)
                        for nm, o, k, s in zip(self.names, self.offsets, self.numels, self.shapes)}
@@ -201,17 +214,15 @@ class StackedState:
         return bad
 
 
-class StackedCSGHMC:
-    """K cyclical-SGHMC chains of `net` on one device, stepped together.
+class _StackedSampler:
+    """What every stacked sampler shares: K chains' state, the vmapped
+    forward/backward (optionally replayed from a HIP graph), the predictive
+    over chains and collected posterior components, the epoch driver."""
 
-    `args` carries the csghmc Runner's fields (lr, lr_head, epochs,
-    num_cycles, proportion_exploration, ND, hparams with prior_sig,
-    momentum_decay, Ninflate, nd, thin, nst, bias; device).  Chains are
-    keyed chain0 + k (default: rank * K, so chains stay distinct across
-    processes) with Philox seed `seed`."""
+    need_prior = False
 
     def __init__(self, net, K_, args, *, chain0=None, seed=None, init="copy", criterion=None,
-                 per_chain_batches=False, logger=None, graph=None):
+                 per_chain_batches=False, logger=None, graph=None, net0=None):
         from . import chains
         from ._base import default_graph
         self.args, self.logger = args, logger
@@ -222,22 +233,17 @@ class StackedCSGHMC:
         hp = args.hparams
         self.net = net.to(args.device)
         self.prior_sig = float(hp["prior_sig"])
-        self.momentum_decay = float(hp["momentum_decay"])
         self.Ninflate, self.nd = float(hp["Ninflate"]), float(hp["nd"])
         self.thin, self.nst = int(hp["thin"]), int(hp["nst"])
         self.seed = int(getattr(args, "seed", 0) or 0) if seed is None else int(seed)
         self.chain0 = chains.rank() * K_ if chain0 is None else int(chain0)
         # re-initialisation seeds seed + chain id: distinct across processes too
         self.state = StackedState(self.net, K_, bias=str(hp["bias"]), init=init,
-                                  seed=self.seed + self.chain0)
+                                  seed=self.seed + self.chain0, need_prior=self.need_prior,
+                                  net0=net0)
         self.K = K_
         self.criterion = criterion or torch.nn.CrossEntropyLoss()
-        self.sched = CyclicalSGMCMC(base_lr=args.lr, nbr_of_cycles=getattr(args, "num_cycles", 10),
-                                    epochs=args.epochs,
-                                    proportion_exploration=getattr(args, "proportion_exploration",
-                                                                   0.5))
         self.step_count = 0
-        self.samples_per_cycle, self.mom1, self.mom2 = {}, {}, {}
         self.draws = 0
         st = self.state
         self.trainable = [nm for nm, rg in zip(st.names, st.requires_grad) if rg]
@@ -296,13 +302,120 @@ class StackedCSGHMC:
         graph.replay()
         return grads, loss, out
 
-    def step(self, x, y, lr, should_sample=False, collect=None):
-        """One cSGHMC step of all K chains (methods/csghmc.py:673-780 per chain):
-        vmapped forward/backward, then one fused launch.  Returns per-chain
-        (loss [K], logits [K, B, C]) on the device, without a host sync."""
+    def step(self, x, y, *a, **kw):
+        """One step of all K chains: vmapped forward/backward, then one fused
+        launch (`update`).  Returns per-chain (loss [K], logits [K, B, C]) on
+        the device, without a host sync."""
         grads, loss, out = self.gradients(x, y)
-        self.update(grads, lr, should_sample, collect)
+        self.update(grads, *a, **kw)
         return loss, out
+
+    def _accumulate(self, acc, loss, out, y):
+        """Per-chain running (loss sum, error count, examples) on the device."""
+        bs = y.shape[-1]
+        acc[0] += loss.double() * bs
+        acc[1] += out.argmax(-1).ne(y).sum(-1)
+        acc[2] += bs
+
+    def _new_acc(self):
+        dev = self.args.device
+        return [torch.zeros(self.K, dtype=torch.float64, device=dev),
+                torch.zeros(self.K, dtype=torch.int64, device=dev), 0]
+
+    @staticmethod
+    def _epoch_result(acc):
+        nb = max(acc[2], 1)
+        return (acc[0] / nb).cpu().numpy(), (acc[1].double() / nb).cpu().numpy()
+
+    # ----------------------------------------------------------- predictive
+    def chain_logits(self, x):
+        """[K, B, C] logits of every chain at its current theta."""
+        with torch.no_grad():
+            return self._fwd(self.state.params, x)
+
+    def predictive_logprob(self, x):
+        """log of the predictive probability averaged uniformly over the K
+        chains x the collected posterior components (`_components`: posterior
+        draws or means); the chains' current theta while none is collected.
+        With one process per GPU (torch.distributed initialised) the
+        processes' stacked predictives are averaged too
+        (chains.average_predictive: one all-reduce)."""
+        from . import chains
+        lp = self._local_logprob(x)
+        return chains.average_predictive(lp) if chains.world() > 1 else lp
+
+    def _local_logprob(self, x):
+        st = self.state
+        with torch.no_grad():
+            buf = torch.empty_like(st.theta)
+            views = {nm: buf.view(self.K, st.stride)[:, o:o + k].view(self.K, *s)
+                     for nm, o, k, s in zip(st.names, st.offsets, st.numels, st.shapes)}
+            comps = [F.log_softmax(self._fwd(views, x), dim=-1) for _ in self._components(buf)]
+            if not comps:
+                comps = [F.log_softmax(self.chain_logits(x), dim=-1)]
+            lp = torch.cat(comps, 0)  # [K * components, B, C]
+            return lp.logsumexp(0) - math.log(lp.shape[0])
+
+    def _sample(self, out, mean, m2, var_mode, ratio):
+        """One posterior draw of every chain into `out` ([K*stride]); chain k
+        keyed chain0 + k (= the one-chain PosteriorDraw of that chain id)."""
+        K.posterior_sample(out, mean, m2, var_mode=var_mode, ratio=ratio, seed=self.seed,
+                           chain=self.chain0, step=EVAL_STEP_BASE + self.draws,
+                           chain_groups=self.state.chain_groups)
+        self.draws += 1
+
+    def evaluate(self, loader):
+        """(NLL, error) of the stacked predictive over a data loader."""
+        dev = self.args.device
+        loss, err, nb = 0.0, 0, 0
+        for x, y in loader:
+            x, y = x.to(dev), y.to(dev)
+            lp = self.predictive_logprob(x)
+            loss += F.nll_loss(lp, y, reduction="sum").item()
+            err += lp.argmax(-1).ne(y).sum().item()
+            nb += len(y)
+        return loss / nb, err / nb
+
+    def train(self, train_loader, test_loader=None):
+        """Run args.epochs epochs; logs per-chain losses and, after the
+        epochs `_evaluate_after` names, the stacked predictive on test_loader."""
+        log = self.logger.info if self.logger is not None else (lambda *_: None)
+        hist = []
+        for ep in range(self.args.epochs):
+            tic = time.time()
+            lt, et = self.train_one_epoch(train_loader, ep)
+            if self.state.diverged():
+                log(f"[Epoch {ep}] a chain wrote a non-finite theta")
+            rec = {"epoch": ep, "loss": lt.tolist(), "error": et.tolist(),
+                   "seconds": time.time() - tic}
+            log(f"[Epoch {ep}/{self.args.epochs}] {self.K} chains: loss = {lt.mean():.4f} "
+                f"(min {lt.min():.4f}, max {lt.max():.4f}), error = {et.mean():.4f} "
+                f"({rec['seconds']:.2f} s)")
+            if test_loader is not None and self._evaluate_after(ep, train_loader):
+                rec["test"] = self.evaluate(test_loader)
+                log(f"(Epoch {ep}) stacked predictive: loss = {rec['test'][0]:.4f}, "
+                    f"error = {rec['test'][1]:.4f}")
+            hist.append(rec)
+        return hist
+
+
+class StackedCSGHMC(_StackedSampler):
+    """K cyclical-SGHMC chains of `net` on one device, stepped together.
+
+    `args` carries the csghmc Runner's fields (lr, lr_head, epochs,
+    num_cycles, proportion_exploration, ND, hparams with prior_sig,
+    momentum_decay, Ninflate, nd, thin, nst, bias; device).  Chains are
+    keyed chain0 + k (default: rank * K, so chains stay distinct across
+    processes) with Philox seed `seed`."""
+
+    def __init__(self, net, K_, args, **kw):
+        super().__init__(net, K_, args, **kw)
+        self.momentum_decay = float(args.hparams["momentum_decay"])
+        self.sched = CyclicalSGMCMC(base_lr=args.lr, nbr_of_cycles=getattr(args, "num_cycles", 10),
+                                    epochs=args.epochs,
+                                    proportion_exploration=getattr(args, "proportion_exploration",
+                                                                   0.5))
+        self.samples_per_cycle, self.mom1, self.mom2 = {}, {}, {}
 
     def update(self, grads, lr, should_sample=False, collect=None):
         """The fused launch over all chains for given gradients (step's second
@@ -339,9 +452,7 @@ class StackedCSGHMC:
         dev, sched = self.args.device, self.sched
         sched.current_epoch = epoch
         bpe = len(loader)
-        loss_sum = torch.zeros(self.K, dtype=torch.float64, device=dev)
-        err_sum = torch.zeros(self.K, dtype=torch.int64, device=dev)
-        nb = 0
+        acc = self._new_acc()
         for b, (x, y) in enumerate(loader):
             x, y = x.to(dev, non_blocking=True), y.to(dev, non_blocking=True)
             lr = sched.calculate_lr(epoch=epoch, batch=b, batches_per_epoch=bpe)
@@ -354,94 +465,110 @@ class StackedCSGHMC:
             loss, out = self.step(x, y, lr, should_sample=ss, collect=collect)
             if ss:  # Q2: the reference bumps the count twice per sample
                 self.samples_per_cycle[c] = cnt + 1
-            bs = y.shape[-1]
-            loss_sum += loss.double() * bs
-            err_sum += out.argmax(-1).ne(y).sum(-1)
-            nb += bs
-        return (loss_sum / nb).cpu().numpy(), (err_sum.double() / nb).cpu().numpy()
+            self._accumulate(acc, loss, out, y)
+        return self._epoch_result(acc)
 
-    # ----------------------------------------------------------- predictive
-    def chain_logits(self, x):
-        """[K, B, C] logits of every chain at its current theta."""
-        with torch.no_grad():
-            return self._fwd(self.state.params, x)
+    def _components(self, buf):
+        """Every collected cycle: nst posterior draws (its Welford mean and
+        variance M2/(n-1), 1e-12 for a single sample; methods/csghmc.py:446-468)
+        or, with nst = 0, its mean."""
+        for c in sorted(self.mom1):
+            n = self.samples_per_cycle.get(c, 0)
+            for _ in range(max(1, self.nst)):
+                if self.nst == 0:
+                    buf.copy_(self.mom1[c])
+                elif n > 1:
+                    self._sample(buf, self.mom1[c], self.mom2[c], L.VAR_WELFORD, float(n - 1))
+                else:
+                    self._sample(buf, self.mom1[c], None, L.VAR_GIVEN, 1.0)
+                yield c
 
-    def _draw_params(self, c, out):
-        """Fill `out` ([K*stride]) with one posterior draw of every chain from
-        cycle c's Welford moments (methods/csghmc.py:446-468; var = M2/(n-1),
-        1e-12 for a single sample), chain k keyed chain0 + k."""
+    def _evaluate_after(self, ep, loader):
+        return self.sched.last_in_cycle(epoch=ep, batch=len(loader) - 1,
+                                        batches_per_epoch=len(loader))
+
+
+class StackedSGLD(_StackedSampler):
+    """K SGLD chains of `net` on one device (methods/sgld.py:69-250 per chain):
+    sampler gradient g + (theta - theta0)/sigma^2/N + nd*sqrt(2/(N lr))*eps,
+    then torch.optim.SGD(momentum=args.momentum) — one fused launch for all
+    chains — with the running posterior moments (m1, m2) after burn-in every
+    `thin` iterations fused into the same sweep.  `args` carries the sgld
+    Runner's fields (lr, lr_head, epochs, momentum, ND, hparams with
+    prior_sig, Ninflate, nd, burnin, thin, nst, bias; device); `net0` is the
+    prior mean (zeros when None)."""
+
+    need_prior = True
+
+    def __init__(self, net, K_, args, **kw):
+        super().__init__(net, K_, args, **kw)
+        self.burnin = int(args.hparams["burnin"])
+        self.mu = float(getattr(args, "momentum", 0.0))
+        self.has_buffer = False
+        self.bi = 0                      # global iteration count thinning uses
+        self.m1 = self.m2 = None
+        self.cnt = 0
+
+    def update(self, grads, lrs, collect=None):
+        """The fused SGLD + SGD(momentum mu) launch over all chains
+        (methods/sgld.py:469-484 + :226), optional running-moment collect."""
+        args, st = self.args, self.state
+        st.use_grads(grads)
+        N = args.ND * self.Ninflate
+        ns = [self.nd * np.sqrt(2 / (N * v)) for v in lrs]
+        mom = self.mu != 0
+        ckind, m1, m2, ca, cb = (L.COLLECT_NONE, None, None, 1.0, 1.0) if collect is None \
+            else collect
+        K.sgmcmc_step(st, L.SGLD, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_PHILOX,
+                      prior_sig=self.prior_sig, sigma2=self.prior_sig ** 2, n_data=N, mu=self.mu,
+                      first_step=mom and not self.has_buffer, momentum=mom, collect=ckind,
+                      mom1=m1, mom2=m2, collect_a=ca, collect_b=cb, seed=self.seed,
+                      chain=self.chain0, step=self.step_count)
+        self.has_buffer = self.has_buffer or mom
+        self.step_count += 1
+
+    def seed_moments(self):
+        """methods/sgld.py:95-102 at the end of burn-in: m1 = theta,
+        m2 = theta^2, count 1 (one stand-alone sweep over all chains)."""
         st = self.state
-        n = self.samples_per_cycle.get(c, 0)
-        if n > 1:
-            m2, vm, ratio = self.mom2[c], L.VAR_WELFORD, float(n - 1)
-        else:
-            m2, vm, ratio = None, L.VAR_GIVEN, 1.0
-        K.posterior_sample(out, self.mom1[c], m2, var_mode=vm, ratio=ratio, seed=self.seed,
-                           chain=self.chain0, step=EVAL_STEP_BASE + self.draws,
-                           chain_groups=st.chain_groups)
-        self.draws += 1
+        self.m1 = torch.empty_like(st.theta)
+        self.m2 = torch.empty_like(st.theta) if self.nst > 0 else None
+        K.moments_update(st.theta, self.m1, self.m2, L.COLLECT_MEAN_INIT)
+        self.cnt = 1
 
-    def predictive_logprob(self, x):
-        """log of the predictive probability averaged uniformly over the K
-        chains x (nst draws of) every collected cycle; the chains' current
-        theta while no cycle has been collected.  With one process per GPU
-        (torch.distributed initialised) the processes' stacked predictives are
-        averaged too (chains.average_predictive: one all-reduce)."""
-        from . import chains
-        lp = self._local_logprob(x)
-        return chains.average_predictive(lp) if chains.world() > 1 else lp
-
-    def _local_logprob(self, x):
-        st = self.state
-        with torch.no_grad():
-            if not self.mom1:
-                lp = F.log_softmax(self.chain_logits(x), dim=-1)
-                return lp.logsumexp(0) - math.log(self.K)
-            buf = torch.empty_like(st.theta)
-            views = {nm: buf.view(self.K, st.stride)[:, o:o + k].view(self.K, *s)
-                     for nm, o, k, s in zip(st.names, st.offsets, st.numels, st.shapes)}
-            comps = []
-            for c in sorted(self.mom1):
-                for _ in range(max(1, self.nst)):
-                    if self.nst == 0:
-                        buf.copy_(self.mom1[c])
-                    else:
-                        self._draw_params(c, buf)
-                    comps.append(F.log_softmax(self._fwd(views, x), dim=-1))
-            lp = torch.cat(comps, 0)  # [K * draws, B, C]
-            return lp.logsumexp(0) - math.log(lp.shape[0])
-
-    def evaluate(self, loader):
-        """(NLL, error) of the stacked predictive over a data loader."""
-        dev = self.args.device
-        loss, err, nb = 0.0, 0, 0
+    def train_one_epoch(self, loader, epoch):
+        args, dev = self.args, self.args.device
+        if epoch == self.burnin:
+            self.seed_moments()
+        collect = epoch >= self.burnin
+        lrs = (args.lr, args.lr_head)
+        acc = self._new_acc()
         for x, y in loader:
-            x, y = x.to(dev), y.to(dev)
-            lp = self.predictive_logprob(x)
-            loss += F.nll_loss(lp, y, reduction="sum").item()
-            err += lp.argmax(-1).ne(y).sum().item()
-            nb += len(y)
-        return loss / nb, err / nb
+            x, y = x.to(dev, non_blocking=True), y.to(dev, non_blocking=True)
+            spec = None
+            do_collect = collect and (self.bi + 1) % self.thin == 0
+            if do_collect:  # methods/sgld.py:239-246
+                spec = (L.COLLECT_MEAN, self.m1, self.m2, float(self.cnt), float(self.cnt + 1))
+            loss, out = self.step(x, y, lrs, collect=spec)
+            if do_collect:
+                self.cnt += 1
+            self.bi += 1
+            self._accumulate(acc, loss, out, y)
+        return self._epoch_result(acc)
 
-    def train(self, train_loader, test_loader=None):
-        """Run args.epochs epochs; logs per-chain losses and, after every
-        epoch that ends a cycle, the stacked predictive on test_loader."""
-        log = self.logger.info if self.logger is not None else (lambda *_: None)
-        hist = []
-        for ep in range(self.args.epochs):
-            tic = time.time()
-            lt, et = self.train_one_epoch(train_loader, ep)
-            if self.state.diverged():
-                log(f"[Epoch {ep}] a chain wrote a non-finite theta")
-            rec = {"epoch": ep, "loss": lt.tolist(), "error": et.tolist(),
-                   "seconds": time.time() - tic}
-            log(f"[Epoch {ep}/{self.args.epochs}] {self.K} chains: loss = {lt.mean():.4f} "
-                f"(min {lt.min():.4f}, max {lt.max():.4f}), error = {et.mean():.4f} "
-                f"({rec['seconds']:.2f} s)")
-            if test_loader is not None and self.sched.last_in_cycle(
-                    epoch=ep, batch=len(train_loader) - 1, batches_per_epoch=len(train_loader)):
-                rec["test"] = self.evaluate(test_loader)
-                log(f"(Epoch {ep}) stacked predictive: loss = {rec['test'][0]:.4f}, "
-                    f"error = {rec['test'][1]:.4f}")
-            hist.append(rec)
-        return hist
+    def _components(self, buf):
+        """nst posterior draws, var = cnt/(cnt-1) * (m2 - m1^2) (1.0 for one
+        sample; methods/sgld.py:324-350), or the posterior mean (nst = 0)."""
+        if self.m1 is None:
+            return
+        for _ in range(max(1, self.nst)):
+            if self.nst == 0:
+                buf.copy_(self.m1)
+            else:
+                ratio = self.cnt / (self.cnt - 1) if self.cnt > 1 else 1.0
+                self._sample(buf, self.m1, self.m2, L.VAR_RAW_MOMENTS, ratio)
+            yield 0
+
+    def _evaluate_after(self, ep, loader):
+        freq = int(getattr(self.args, "test_eval_freq", 1) or 1)
+        return ep >= self.burnin and ((ep + 1) % freq == 0 or ep + 1 == self.args.epochs)

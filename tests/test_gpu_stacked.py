@@ -191,6 +191,84 @@ def test_stacked_graph_replay_is_bit_identical_to_eager():
         assert torch.equal(a, b)
 
 
+def test_stacked_sgld_equals_one_chain_launches():
+    """StackedSGLD (SGLD + SGD momentum, prior theta0 from net0, burn-in
+    seeding, running moments): every chain equals a one-chain SGLD launch
+    sequence with chain id chain0 + k, bit for bit, given the same gradients."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd import stacked
+    from bayesdll_amd.flat import FlatState
+    torch.manual_seed(5)
+    K_ = 3
+    args = _args()
+    args.momentum = 0.5
+    args.hparams.update({"Ninflate": 10.0, "burnin": 0, "thin": 2, "nst": 2})
+    net0 = Net().cuda()
+    S = stacked.StackedSGLD(Net().cuda(), K_, args, chain0=2, init="reinit", net0=net0)
+    st = S.state
+    segs = [(nm, sh) for nm, sh in zip(st.names, st.shapes)]
+    singles = []
+    for k in range(K_):
+        one = FlatState.from_segments(segs, "head", device="cuda", need_mom=True, need_prior=True,
+                                      init=st.chain_vector(k).clone())
+        one.prior.copy_(st.prior.view(K_, -1)[k, :st.n1])
+        singles.append(one)
+    S.seed_moments()
+    m1s = [S.m1.view(K_, -1)[k, :st.n1].clone() for k in range(K_)]
+    m2s = [S.m2.view(K_, -1)[k, :st.n1].clone() for k in range(K_)]
+    x = torch.randn(16, 13, device="cuda")
+    y = torch.randint(0, 5, (16,), device="cuda")
+    lrs = (args.lr, args.lr_head)
+    N = args.ND * 10.0
+    for t in range(5):
+        grads, _, _ = S.gradients(x, y)
+        collect = t % 2 == 1
+        spec = (L.COLLECT_MEAN, S.m1, S.m2, float(S.cnt), float(S.cnt + 1)) if collect else None
+        cnt = S.cnt
+        S.update(grads, lrs, collect=spec)
+        if collect:
+            S.cnt += 1
+        for k, one in enumerate(singles):
+            one.use_tensor_grads([grads[nm][k].contiguous().view(-1) for nm in st.names])
+            K.sgmcmc_step(one, L.SGLD, lrs=lrs, noise_scale=[np.sqrt(2 / (N * v)) for v in lrs],
+                          noise_mode=L.NOISE_PHILOX, prior_sig=1.0, sigma2=1.0, n_data=N, mu=0.5,
+                          first_step=t == 0, momentum=True,
+                          collect=L.COLLECT_MEAN if collect else L.COLLECT_NONE,
+                          mom1=m1s[k] if collect else None, mom2=m2s[k] if collect else None,
+                          collect_a=float(cnt), collect_b=float(cnt + 1), seed=S.seed,
+                          chain=2 + k, step=t)
+    torch.cuda.synchronize()
+    for k, one in enumerate(singles):
+        assert torch.equal(st.theta2d[k, :st.n1], one.theta), k
+        assert torch.equal(st.mom2d[k, :st.n1], one.mom), k
+        assert torch.equal(S.m1.view(K_, -1)[k, :st.n1], m1s[k]), k
+        assert torch.equal(S.m2.view(K_, -1)[k, :st.n1], m2s[k]), k
+    # the prior is net0 in every chain's slot
+    p0 = torch.cat([q.detach().reshape(-1) for q in net0.parameters()])
+    assert all(torch.equal(st.prior.view(K_, -1)[k, :st.n1], p0) for k in range(K_))
+
+
+def test_stacked_sgld_trains_and_evaluates():
+    from bayesdll_amd import stacked
+    torch.manual_seed(6)
+    w = torch.randn(13, 5)
+    xs = torch.randn(512, 13)
+    ys = (xs @ w).argmax(1)
+    loader = [(xs[i:i + 32], ys[i:i + 32]) for i in range(0, 512, 32)]
+    args = _args(epochs=4, nst=3)
+    args.lr, args.lr_head, args.ND, args.momentum = 0.2, 0.2, 512, 0.5  # CPU emulation: 0.55 -> 0.12
+    args.hparams.update({"prior_sig": 1.0, "Ninflate": 1e3, "nd": 1.0, "burnin": 2, "thin": 2})
+    S = stacked.StackedSGLD(Net().cuda(), 6, args, init="reinit", seed=2, graph=True)
+    hist = S.train(loader, test_loader=loader)
+    first, last = np.array(hist[0]["error"]), np.array(hist[-1]["error"])
+    assert last.mean() < 0.5 * first.mean() and last.max() < 0.3
+    assert S.cnt == 1 + (2 * 16) // 2 and "test" not in hist[1] and "test" in hist[3]
+    nll, err = S.evaluate(loader)
+    assert np.isfinite(nll) and err < 0.3
+    assert not S.state.diverged()
+
+
 def test_stacked_refuses_batchnorm_statistics():
     from bayesdll_amd import stacked
     net = nn.Sequential(nn.Linear(4, 4), nn.BatchNorm1d(4)).cuda()
