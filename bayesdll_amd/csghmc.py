@@ -224,6 +224,7 @@ class Runner:
                         self.save_ckpt(epoch=sched.current_epoch)
                     self._cycle_completed(cycle_number)
         error = int(torch.stack(errs).sum().item()) if errs else 0
+        self.model.defer_loss = False  # Model called directly: loss.item() again
         return float(loss) / nb_samples, error / nb_samples, cycle_updated
 
     def _cycle_completed(self, cycle_number):

@@ -205,6 +205,7 @@ class Runner:
                         self.save_ckpt(epoch=sched.current_epoch)
                     self._cycle_completed(cycle_number)
         error = int(torch.stack(errs).sum().item()) if errs else 0
+        self.model.defer_loss = False  # Model called directly: loss.item() again
         return float(loss) / nb, error / nb, cycle_updated
 
     def _variance_source(self, cycle):

@@ -198,6 +198,7 @@ class Runner:
                 logger.info("(post-burnin) accumulate posterior samples")
                 self.post_theta_cnt += 1
         error = int(torch.stack(errs).sum().item()) if errs else 0
+        self.model.defer_loss = False  # Model called directly: loss.item() again
         return float(loss) / nb, error / nb, bi
 
     # --------------------------------------------------------------- evaluate

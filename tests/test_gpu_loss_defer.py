@@ -43,6 +43,6 @@ def test_deferred_epoch_loss_equals_per_step_sum(method, monkeypatch, tmp_path):
         res = [R.train_one_epoch(loader) if method != "sgld" else
                R.train_one_epoch(loader, False, 0) for _ in range(2)]
         out[sync] = [(float(r[0]), float(r[1])) for r in res]
-        assert R.model.defer_loss == (sync == "0")
+        assert not R.model.defer_loss  # reset after the epoch: direct calls get floats
         assert all(type(r[0]) is float for r in res)
     assert out["1"] == out["0"]
