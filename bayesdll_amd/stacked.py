@@ -376,12 +376,47 @@ class _StackedSampler:
             nb += len(y)
         return loss / nb, err / nb
 
-    def train(self, train_loader, test_loader=None):
-        """Run args.epochs epochs; logs per-chain losses and, after the
-        epochs `_evaluate_after` names, the stacked predictive on test_loader."""
+    # ---------------------------------------------------------- checkpoint
+    def state_dict(self):
+        """Everything an exact continuation of all K chains needs: the stacked
+        theta / momentum / prior, the sampler's step counter (the Philox step
+        key), draw counter and the method's moments and counters."""
+        st = self.state
+        d = {"stacked": type(self).__name__, "K": self.K, "chain0": self.chain0,
+             "seed": self.seed, "n": st.n1, "stride": st.stride, "theta": st.theta,
+             "mom": st.mom, "prior": st.prior, "step_count": self.step_count,
+             "draws": self.draws}
+        d.update(self._extra_state())
+        return d
+
+    def save_ckpt(self, path):
+        torch.save(self.state_dict(), path)
+        return path
+
+    def load_ckpt(self, path):
+        """Restore a save_ckpt file (weights-only load) into this sampler."""
+        d = torch.load(path, map_location=self.state.device, weights_only=True)
+        st = self.state
+        if (d.get("stacked") != type(self).__name__ or d["K"] != self.K or d["n"] != st.n1
+                or d["stride"] != st.stride):
+            raise ValueError("load_ckpt: checkpoint of a different stacked sampler / network")
+        with torch.no_grad():
+            st.theta.copy_(d["theta"])
+            for mine, theirs in ((st.mom, d["mom"]), (st.prior, d["prior"])):
+                if mine is not None and theirs is not None:
+                    mine.copy_(theirs)
+        self.chain0, self.seed = d["chain0"], d["seed"]
+        self.step_count, self.draws = d["step_count"], d["draws"]
+        self._load_extra_state(d)
+        return d
+
+    def train(self, train_loader, test_loader=None, start_epoch=0):
+        """Run epochs start_epoch .. args.epochs-1 (start_epoch > 0 continues
+        after load_ckpt); logs per-chain losses and, after the epochs
+        `_evaluate_after` names, the stacked predictive on test_loader."""
         log = self.logger.info if self.logger is not None else (lambda *_: None)
         hist = []
-        for ep in range(self.args.epochs):
+        for ep in range(start_epoch, self.args.epochs):
             tic = time.time()
             lt, et = self.train_one_epoch(train_loader, ep)
             if self.state.diverged():
@@ -487,6 +522,30 @@ class StackedCSGHMC(_StackedSampler):
         return self.sched.last_in_cycle(epoch=ep, batch=len(loader) - 1,
                                         batches_per_epoch=len(loader))
 
+    def _extra_state(self):
+        return {"samples_per_cycle": dict(self.samples_per_cycle), "mom1": dict(self.mom1),
+                "mom2": dict(self.mom2), "epoch": self.sched.current_epoch}
+
+    def _load_extra_state(self, d):
+        self.samples_per_cycle = dict(d["samples_per_cycle"])
+        self.mom1, self.mom2 = dict(d["mom1"]), dict(d["mom2"])
+        self.sched.current_epoch = d["epoch"]
+
+    def export_chain(self, k, epoch=None):
+        """Chain k as a one-chain csghmc checkpoint (the keys of
+        methods/csghmc.py:530-549 / bayesdll_amd.csghmc.Runner.save_ckpt, flat
+        vectors in parameters_to_vector order): `torch.save` it and a
+        Runner's load_ckpt takes it."""
+        st, n1 = self.state, self.state.n1
+        sl = (lambda v: v.view(self.K, st.stride)[k, :n1].clone())
+        return {"last_theta": st.chain_vector(k).clone(),
+                "cycle_theta_mom1": {c: sl(v) for c, v in self.mom1.items()},
+                "cycle_theta_mom2": {c: sl(v) for c, v in self.mom2.items()},
+                "cycle_likelihoods": {}, "cycle_states": {},
+                "epoch": self.sched.current_epoch if epoch is None else epoch,
+                "current_cycle": max(self.mom1) if self.mom1 else 0,
+                "samples_per_cycle": dict(self.samples_per_cycle)}
+
 
 class StackedSGLD(_StackedSampler):
     """K SGLD chains of `net` on one device (methods/sgld.py:69-250 per chain):
@@ -572,3 +631,11 @@ class StackedSGLD(_StackedSampler):
     def _evaluate_after(self, ep, loader):
         freq = int(getattr(self.args, "test_eval_freq", 1) or 1)
         return ep >= self.burnin and ((ep + 1) % freq == 0 or ep + 1 == self.args.epochs)
+
+    def _extra_state(self):
+        return {"m1": self.m1, "m2": self.m2, "cnt": self.cnt, "bi": self.bi,
+                "has_buffer": self.has_buffer}
+
+    def _load_extra_state(self, d):
+        self.m1, self.m2 = d["m1"], d["m2"]
+        self.cnt, self.bi, self.has_buffer = d["cnt"], d["bi"], d["has_buffer"]

@@ -269,6 +269,58 @@ def test_stacked_sgld_trains_and_evaluates():
     assert not S.state.diverged()
 
 
+@pytest.mark.parametrize("cls", ["StackedCSGHMC", "StackedSGLD"])
+def test_stacked_checkpoint_resume_is_exact(cls, tmp_path):
+    """Two epochs, save_ckpt, two more epochs == a fresh sampler that loads the
+    checkpoint and runs the last two epochs (theta, momentum, moments, bit for
+    bit: the step counter is the Philox step key)."""
+    from bayesdll_amd import stacked
+    g = torch.Generator().manual_seed(8)
+    xs, ys = torch.randn(256, 13, generator=g), torch.randint(0, 5, (256,), generator=g)
+    loader = [(xs[i:i + 32].cuda(), ys[i:i + 32].cuda()) for i in range(0, 256, 32)]
+    args = _args(epochs=4, nst=2)
+    args.momentum = 0.5
+    args.hparams.update({"burnin": 1, "thin": 2})
+
+    def make():
+        torch.manual_seed(11)
+        return getattr(stacked, cls)(Net().cuda(), 3, args, init="reinit", seed=4, chain0=0)
+
+    A = make()
+    for ep in range(2):
+        A.train_one_epoch(loader, ep)
+    path = A.save_ckpt(str(tmp_path / "stacked.pt"))
+    for ep in range(2, 4):
+        A.train_one_epoch(loader, ep)
+    B = make()
+    B.load_ckpt(path)
+    B.train(loader, start_epoch=2)
+    torch.cuda.synchronize()
+    assert torch.equal(A.state.theta, B.state.theta)
+    assert torch.equal(A.state.mom, B.state.mom)
+    if cls == "StackedCSGHMC":
+        assert sorted(A.mom1) == sorted(B.mom1) == [1, 2]
+        for c in A.mom1:
+            assert torch.equal(A.mom1[c], B.mom1[c]) and torch.equal(A.mom2[c], B.mom2[c])
+        assert A.samples_per_cycle == B.samples_per_cycle
+        # chain 1 as a one-chain csghmc checkpoint the Runner loads
+        from bayesdll_amd import csghmc
+        ck = A.export_chain(1)
+        torch.save(ck, tmp_path / "chain1.pt")
+        args.pretrained = None
+        R = csghmc.Runner(Net().cuda(), None, args, __import__("logging").getLogger("t"))
+        R.load_ckpt(str(tmp_path / "chain1.pt"))
+        n1 = A.state.n1
+        assert torch.equal(ck["last_theta"], A.state.theta2d[1, :n1])
+        for c in A.mom1:
+            assert torch.equal(R.cycle_theta_mom1[c], A.mom1[c].view(3, -1)[1, :n1])
+        assert R.samples_per_cycle == A.samples_per_cycle
+    else:
+        assert A.cnt == B.cnt and torch.equal(A.m1, B.m1) and torch.equal(A.m2, B.m2)
+    with pytest.raises(ValueError, match="different"):
+        getattr(stacked, cls)(Net().cuda(), 2, args).load_ckpt(path)
+
+
 def test_stacked_refuses_batchnorm_statistics():
     from bayesdll_amd import stacked
     net = nn.Sequential(nn.Linear(4, 4), nn.BatchNorm1d(4)).cuda()
