@@ -365,15 +365,21 @@ class _StackedSampler:
         self.draws += 1
 
     def evaluate(self, loader):
-        """(NLL, error) of the stacked predictive over a data loader."""
+        """(NLL, error) of the stacked predictive over a data loader (the
+        network in eval mode, as the reference's evaluate)."""
         dev = self.args.device
         loss, err, nb = 0.0, 0, 0
-        for x, y in loader:
-            x, y = x.to(dev), y.to(dev)
-            lp = self.predictive_logprob(x)
-            loss += F.nll_loss(lp, y, reduction="sum").item()
-            err += lp.argmax(-1).ne(y).sum().item()
-            nb += len(y)
+        was = self.net.training
+        self.net.eval()
+        try:
+            for x, y in loader:
+                x, y = x.to(dev), y.to(dev)
+                lp = self.predictive_logprob(x)
+                loss += F.nll_loss(lp, y, reduction="sum").item()
+                err += lp.argmax(-1).ne(y).sum().item()
+                nb += len(y)
+        finally:
+            self.net.train(was)
         return loss / nb, err / nb
 
     # ---------------------------------------------------------- checkpoint
