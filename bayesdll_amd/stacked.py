@@ -491,6 +491,7 @@ class StackedCSGHMC(_StackedSampler):
         (methods/csghmc.py:246-384).  Returns per-chain (loss, error) arrays;
         one host sync per epoch."""
         dev, sched = self.args.device, self.sched
+        self.net.train()
         sched.current_epoch = epoch
         bpe = len(loader)
         acc = self._new_acc()
@@ -603,6 +604,7 @@ class StackedSGLD(_StackedSampler):
 
     def train_one_epoch(self, loader, epoch):
         args, dev = self.args, self.args.device
+        self.net.train()
         if epoch == self.burnin:
             self.seed_moments()
         collect = epoch >= self.burnin
