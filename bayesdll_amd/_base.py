@@ -112,7 +112,8 @@ class FusedModelBase(nn.Module):
             # launch geometry for this device and size (speed only: results
             # never depend on it)
             from . import kernels as K
-            K.autotune_once(self._state.n, self._state.device, self.tune_method)
+            self._state.launch_cfg = K.autotune_once(self._state.n, self._state.device,
+                                                     self.tune_method)
         return self._state
 
     @property

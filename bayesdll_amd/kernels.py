@@ -144,6 +144,7 @@ class StepTimer:
 
 
 def _launch(state, fn, a, adam=None):
+    _use_geometry(state)
     t = getattr(state, "timer", None)
     e0 = t.begin() if t is not None else None
     fn()
@@ -208,6 +209,7 @@ def sgld_step_clipped(state, max_norm, **kw):
     pass, a one-workgroup finalize and the update pass.  Returns the workspace
     whose first two floats are (total_norm, clip_coef)."""
     a = _step_args(state, L.SGLD, **kw)
+    _use_geometry(state)
     ws = clip_workspace(state)
     L.check(L.lib().bdl_sgld_step_clipped(a, float(max_norm), ws.data_ptr(),
                                           L.current_stream_handle(state.device)),
@@ -260,8 +262,22 @@ def philox_normal(n, seed, chain, step, device="cuda"):
     return out
 
 
+_ACTIVE = [None]  # the geometry last installed through set_launch_config (None: defaults)
+
+
 def set_launch_config(blocks_per_cu=0, unroll=0, grid_stride=0):
+    _ACTIVE[0] = (int(blocks_per_cu), int(unroll), int(grid_stride))
     return L.lib().bdl_set_launch_config(int(blocks_per_cu), int(unroll), int(grid_stride))
+
+
+def _use_geometry(state):
+    """Install the geometry tuned for this state's size (state.launch_cfg, set
+    from autotune_once) if another state's is active: the library's launch
+    configuration is process-wide, and a process may hold states of very
+    different sizes (e.g. a one-chain sampler and a stacked one)."""
+    cfg = getattr(state, "launch_cfg", None)
+    if cfg is not None and cfg != _ACTIVE[0]:
+        set_launch_config(*cfg)
 
 
 # Launch geometries worth trying on gfx950 (workgroups/CU, float4 groups in

@@ -214,12 +214,18 @@ class StackedState:
         return bad
 
 
+def st_big(st):
+    """Worth tuning the launch geometry for (small sweeps are launch-bound)."""
+    return st.device.type == "cuda" and st.n >= 1 << 20
+
+
 class _StackedSampler:
     """What every stacked sampler shares: K chains' state, the vmapped
     forward/backward (optionally replayed from a HIP graph), the predictive
     over chains and collected posterior components, the epoch driver."""
 
     need_prior = False
+    tune_method = "csghmc"  # the production kernel autotune_once times
 
     def __init__(self, net, K_, args, *, chain0=None, seed=None, init="copy", criterion=None,
                  per_chain_batches=False, logger=None, graph=None, net0=None):
@@ -242,6 +248,10 @@ class _StackedSampler:
                                   seed=self.seed + self.chain0, need_prior=self.need_prior,
                                   net0=net0)
         self.K = K_
+        # launch geometry tuned for the stacked size (speed only)
+        if st_big(self.state):
+            self.state.launch_cfg = K.autotune_once(self.state.n, self.state.device,
+                                                    self.tune_method)
         self.criterion = criterion or torch.nn.CrossEntropyLoss()
         self.step_count = 0
         self.draws = 0
@@ -565,6 +575,7 @@ class StackedSGLD(_StackedSampler):
     prior mean (zeros when None)."""
 
     need_prior = True
+    tune_method = "sgld"
 
     def __init__(self, net, K_, args, **kw):
         super().__init__(net, K_, args, **kw)
