@@ -33,7 +33,7 @@ def kind_of(name):
         return KIND.get((int(m.group(2)), int(m.group(3))))
     if m and int(m.group(1)) == 2:
         return SGLD_KIND.get((int(m.group(2)), int(m.group(3))))
-    m = re.search(r"bdl_adam_kernel<(\d+), (\d+), false>", name)
+    m = re.search(r"bdl_adam_kernel<(\d+), (\d+), false(?:, \d+)?>", name)
     if m:
         return ADAM_KIND.get((int(m.group(1)), int(m.group(2))))
     return None
@@ -77,7 +77,6 @@ def main(tag, dest=None, backbone="vit_l_32"):
         rows = [r for r in csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv")))
                 if "bdl_step_kernel" in r["Kernel_Name"] or "bdl_adam_kernel" in r["Kernel_Name"]]
         rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-        seen = set()
         with open(os.path.join(dst, f"pmc_{sub}.csv"), "w", newline="") as f:
             w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Counter_Name",
                                               "Counter_Value", "VGPR_Count", "SGPR_Count",
@@ -87,11 +86,20 @@ def main(tag, dest=None, backbone="vit_l_32"):
             for r in rows:
                 w.writerow(r)
                 k = kind_of(r["Kernel_Name"])
-                if k in FIRST_OF and k not in seen:  # the run's first step (k == 0)
-                    seen.add(k)
-                    k = FIRST_OF[k]
                 if k:
                     acc.setdefault(k, {}).setdefault(counter, []).append(float(r["Counter_Value"]))
+    # the run's first step (SGD buffer created: no buffer read) is the one
+    # dispatch of its kind with clearly less FETCH; autotune / placement
+    # launches come earlier, so find it by its bytes, not its position
+    for k, first in FIRST_OF.items():
+        d = acc.get(k)
+        if not d or "FETCH_SIZE" not in d or len(d["FETCH_SIZE"]) < 3:
+            continue
+        f = d["FETCH_SIZE"]
+        i = min(range(len(f)), key=f.__getitem__)
+        n = len(f)
+        if f[i] < 0.95 * sorted(f)[n // 2] and all(len(v) == n for v in d.values()):
+            acc[first] = {c: [v.pop(i)] for c, v in d.items()}
     traffic, raw = {}, {}
     for k, d in acc.items():
         raw[k] = {c: sum(v) / len(v) for c, v in d.items()}
