@@ -106,7 +106,7 @@ def build_parser():
     ap.add_argument("--resume_state", action="store_true",
                     help="checkpoints carry what an exact resume needs")
     ap.add_argument("--stacked_chains", type=int, default=0,
-                    help="csghmc / sgld: K > 0 chains per device stepped together "
+                    help="csghmc / sgld / csgld: K > 0 chains per device stepped together "
                          "(bayesdll_amd.stacked; no BatchNorm statistics)")
     return ap
 
@@ -201,9 +201,10 @@ def main(argv=None):
 
     if args.stacked_chains > 0:
         from . import stacked
-        cls = {"csghmc": stacked.StackedCSGHMC, "sgld": stacked.StackedSGLD}.get(args.method)
+        cls = {"csghmc": stacked.StackedCSGHMC, "sgld": stacked.StackedSGLD,
+               "csgld": stacked.StackedCSGLD}.get(args.method)
         if cls is None:
-            raise ValueError("--stacked_chains: csghmc or sgld")
+            raise ValueError("--stacked_chains: csghmc, sgld or csgld")
         S = cls(net, args.stacked_chains, args, logger=logger, init="reinit", graph=args.graph,
                 net0=net0)
         logger.info(f"{args.stacked_chains} stacked chains on this device "

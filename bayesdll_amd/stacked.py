@@ -23,8 +23,9 @@ gradients come from batched GEMMs, so a stacked chain agrees with a separately
 run chain to rounding, not bitwise.
 
 Scope: StackedCSGHMC (the north-star sampler: cyclical schedule, thinning,
-per-cycle Welford moments) and StackedSGLD (SGLD + SGD momentum, prior mean
-theta0, burn-in, thinned running moments); the predictive averages
+per-cycle Welford moments), StackedSGLD (SGLD + SGD momentum, prior mean
+theta0, burn-in, thinned running moments) and StackedCSGLD (cyclical SGLD,
+per-cycle running moments); the predictive averages
 probabilities uniformly over chains and (nst posterior draws of) the collected
 components.  Networks with BatchNorm running statistics are refused (vmap cannot
 update shared buffers per chain), and every trainable parameter must take part
@@ -658,3 +659,74 @@ class StackedSGLD(_StackedSampler):
     def _load_extra_state(self, d):
         self.m1, self.m2 = d["m1"], d["m2"]
         self.cnt, self.bi, self.has_buffer = d["cnt"], d["bi"], d["has_buffer"]
+
+
+class StackedCSGLD(StackedSGLD):
+    """K cyclical-SGLD chains (methods/csgld.py:195-331 per chain): SGLD + SGD
+    momentum under the cyclical step size, per-cycle running moments
+    (m1 = theta, m2 = theta^2 at a cycle's first sample, then the running
+    mean) on the sample steps.  No burn-in; `args` as the csgld Runner's."""
+
+    def __init__(self, net, K_, args, **kw):
+        super().__init__(net, K_, args, **kw)
+        self.burnin = -1  # cSGLD collects per cycle, not after a burn-in
+        self.sched = CyclicalSGMCMC(base_lr=args.lr, nbr_of_cycles=getattr(args, "num_cycles", 10),
+                                    epochs=args.epochs,
+                                    proportion_exploration=getattr(args, "proportion_exploration",
+                                                                   0.5))
+        self.samples_per_cycle, self.mom1, self.mom2 = {}, {}, {}
+
+    def train_one_epoch(self, loader, epoch):
+        args, dev, sched = self.args, self.args.device, self.sched
+        self.net.train()
+        sched.current_epoch = epoch
+        bpe = len(loader)
+        acc = self._new_acc()
+        st = self.state
+        for b, (x, y) in enumerate(loader):
+            x, y = x.to(dev, non_blocking=True), y.to(dev, non_blocking=True)
+            lr = sched.calculate_lr(epoch=epoch, batch=b, batches_per_epoch=bpe)
+            ss = sched.should_sample(epoch=epoch, batch=b, batches_per_epoch=bpe) \
+                and b % self.thin == 0
+            spec, c = None, None
+            if ss:  # methods/csgld.py:280-293
+                c = sched.get_cycle_number(epoch=epoch, batch=b, batches_per_epoch=bpe)
+                if c not in self.mom1:
+                    self.mom1[c] = torch.zeros_like(st.theta)
+                    self.mom2[c] = torch.zeros_like(st.theta)
+                    spec = (L.COLLECT_MEAN_INIT, self.mom1[c], self.mom2[c], 1.0, 1.0)
+                else:
+                    cc = self.samples_per_cycle.get(c, 0) + 1
+                    spec = (L.COLLECT_MEAN, self.mom1[c], self.mom2[c], float(cc - 1), float(cc))
+            loss, out = self.step(x, y, (lr, lr * (args.lr_head / args.lr)), collect=spec)
+            if ss:
+                self.samples_per_cycle[c] = self.samples_per_cycle.get(c, 0) + 1
+            self._accumulate(acc, loss, out, y)
+        return self._epoch_result(acc)
+
+    def _components(self, buf):
+        """Every collected cycle: nst draws with var = spc/(spc-1) * (m2 - m1^2)
+        (ratio 1 for a one-sample cycle; methods/csgld.py:394-400), or its mean."""
+        for c in sorted(self.mom1):
+            spc = self.samples_per_cycle.get(c, 0)
+            for _ in range(max(1, self.nst)):
+                if self.nst == 0:
+                    buf.copy_(self.mom1[c])
+                else:
+                    self._sample(buf, self.mom1[c], self.mom2[c], L.VAR_RAW_MOMENTS,
+                                 spc / (spc - 1) if spc > 1 else 1.0)
+                yield c
+
+    def _evaluate_after(self, ep, loader):
+        return self.sched.last_in_cycle(epoch=ep, batch=len(loader) - 1,
+                                        batches_per_epoch=len(loader))
+
+    def _extra_state(self):
+        return {"samples_per_cycle": dict(self.samples_per_cycle), "mom1": dict(self.mom1),
+                "mom2": dict(self.mom2), "has_buffer": self.has_buffer,
+                "epoch": self.sched.current_epoch}
+
+    def _load_extra_state(self, d):
+        self.samples_per_cycle = dict(d["samples_per_cycle"])
+        self.mom1, self.mom2 = dict(d["mom1"]), dict(d["mom2"])
+        self.has_buffer, self.sched.current_epoch = d["has_buffer"], d["epoch"]

@@ -269,7 +269,7 @@ def test_stacked_sgld_trains_and_evaluates():
     assert not S.state.diverged()
 
 
-@pytest.mark.parametrize("cls", ["StackedCSGHMC", "StackedSGLD"])
+@pytest.mark.parametrize("cls", ["StackedCSGHMC", "StackedSGLD", "StackedCSGLD"])
 def test_stacked_checkpoint_resume_is_exact(cls, tmp_path):
     """Two epochs, save_ckpt, two more epochs == a fresh sampler that loads the
     checkpoint and runs the last two epochs (theta, momentum, moments, bit for
@@ -315,10 +315,38 @@ def test_stacked_checkpoint_resume_is_exact(cls, tmp_path):
         for c in A.mom1:
             assert torch.equal(R.cycle_theta_mom1[c], A.mom1[c].view(3, -1)[1, :n1])
         assert R.samples_per_cycle == A.samples_per_cycle
+    elif cls == "StackedCSGLD":
+        assert sorted(A.mom1) == sorted(B.mom1) == [1, 2]
+        for c in A.mom1:
+            assert torch.equal(A.mom1[c], B.mom1[c]) and torch.equal(A.mom2[c], B.mom2[c])
+        assert A.samples_per_cycle == B.samples_per_cycle
     else:
         assert A.cnt == B.cnt and torch.equal(A.m1, B.m1) and torch.equal(A.m2, B.m2)
     with pytest.raises(ValueError, match="different"):
         getattr(stacked, cls)(Net().cuda(), 2, args).load_ckpt(path)
+
+
+def test_stacked_csgld_trains_and_evaluates():
+    """Cyclical SGLD: per-cycle running moments on the sample steps of each
+    cycle (16 per cycle here), predictive over chains x cycle draws."""
+    from bayesdll_amd import stacked
+    torch.manual_seed(7)
+    w = torch.randn(13, 5)
+    xs = torch.randn(512, 13)
+    ys = (xs @ w).argmax(1)
+    loader = [(xs[i:i + 32], ys[i:i + 32]) for i in range(0, 512, 32)]
+    args = _args(epochs=4, nst=2)
+    args.lr, args.lr_head, args.ND, args.momentum = 0.2, 0.2, 512, 0.5
+    args.hparams.update({"prior_sig": 1.0, "Ninflate": 1e3, "nd": 1.0, "thin": 1})
+    S = stacked.StackedCSGLD(Net().cuda(), 4, args, init="reinit", seed=3)
+    hist = S.train(loader, test_loader=loader)
+    assert S.samples_per_cycle == {1: 16, 2: 16} and sorted(S.mom1) == [1, 2]
+    assert "test" in hist[1] and "test" in hist[3] and "test" not in hist[0]
+    first, last = np.array(hist[0]["error"]), np.array(hist[-1]["error"])
+    assert last.mean() < first.mean()
+    nll, err = S.evaluate(loader)
+    assert np.isfinite(nll) and err < 0.5
+    assert not S.state.diverged()
 
 
 def test_stacked_refuses_batchnorm_statistics():
