@@ -11,7 +11,7 @@ Drop-in modules (same Runner/Model interfaces as the reference's methods/*.py):
     bayesdll_amd.cyclical CyclicalSGMCMC  (methods/cyclical.py)
     bayesdll_amd.calibration  ECE / MCE / NLL / temperature (calibration.py)
     bayesdll_amd.chains   one chain per GPU; the cross-chain predictive (RCCL)
-    bayesdll_amd.stacked  K cSGHMC / SGLD / cSGLD chains per device in one launch (not in the reference)
+    bayesdll_amd.stacked  K cSGHMC / SGHMC / SGLD / cSGLD chains per device in one launch (not in the reference)
     bayesdll_amd.run      command-line driver with the demos' flags (demo_mnist.py)
 
 The per-step update runs in hand-written HIP kernels for gfx950

@@ -106,7 +106,7 @@ def build_parser():
     ap.add_argument("--resume_state", action="store_true",
                     help="checkpoints carry what an exact resume needs")
     ap.add_argument("--stacked_chains", type=int, default=0,
-                    help="csghmc / sgld / csgld: K > 0 chains per device stepped together "
+                    help="csghmc / sghmc / sgld / csgld: K > 0 chains per device stepped together "
                          "(bayesdll_amd.stacked; no BatchNorm statistics)")
     return ap
 
@@ -202,9 +202,9 @@ def main(argv=None):
     if args.stacked_chains > 0:
         from . import stacked
         cls = {"csghmc": stacked.StackedCSGHMC, "sgld": stacked.StackedSGLD,
-               "csgld": stacked.StackedCSGLD}.get(args.method)
+               "csgld": stacked.StackedCSGLD, "sghmc": stacked.StackedSGHMC}.get(args.method)
         if cls is None:
-            raise ValueError("--stacked_chains: csghmc, sgld or csgld")
+            raise ValueError("--stacked_chains: csghmc, sghmc, sgld or csgld")
         S = cls(net, args.stacked_chains, args, logger=logger, init="reinit", graph=args.graph,
                 net0=net0)
         logger.info(f"{args.stacked_chains} stacked chains on this device "

@@ -1,4 +1,4 @@
-"""Stacked chains: K independent cSGHMC (or SGLD) chains of one network on one device.
+"""Stacked chains: K independent SG-MCMC chains of one network on one device.
 
 The reference runs one chain per process (methods/csghmc.py:41); its own
 recipe for more chains is more processes.  On an MI355X a small network
@@ -24,8 +24,9 @@ run chain to rounding, not bitwise.
 
 Scope: StackedCSGHMC (the north-star sampler: cyclical schedule, thinning,
 per-cycle Welford moments), StackedSGLD (SGLD + SGD momentum, prior mean
-theta0, burn-in, thinned running moments) and StackedCSGLD (cyclical SGLD,
-per-cycle running moments); the predictive averages
+theta0, burn-in, thinned running moments), StackedSGHMC (the same loop with
+the SGHMC momentum update) and StackedCSGLD (cyclical SGLD, per-cycle running
+moments); the predictive averages
 probabilities uniformly over chains and (nst posterior draws of) the collected
 components.  Networks with BatchNorm running statistics are refused (vmap cannot
 update shared buffers per chain), and every trainable parameter must take part
@@ -730,3 +731,30 @@ class StackedCSGLD(StackedSGLD):
         self.samples_per_cycle = dict(d["samples_per_cycle"])
         self.mom1, self.mom2 = dict(d["mom1"]), dict(d["mom2"])
         self.has_buffer, self.sched.current_epoch = d["has_buffer"], d["epoch"]
+
+
+class StackedSGHMC(StackedSGLD):
+    """K SGHMC chains (methods/sghmc.py:16-512 per chain): momentum
+    v' = v(1-a) + lr-scaled sampler gradient with the prior pull and
+    nd*sqrt(2a/(N lr)) noise, then SGD(momentum 0) on g + v' — one fused
+    launch for all chains — and the SGLD Runner's burn-in / thinned running
+    moments.  `args` as the sghmc Runner's (hparams with momentum_decay)."""
+
+    def __init__(self, net, K_, args, **kw):
+        super().__init__(net, K_, args, **kw)
+        self.momentum_decay = float(args.hparams["momentum_decay"])
+        self.mu = 0.0
+
+    def update(self, grads, lrs, collect=None):
+        args, st = self.args, self.state
+        st.use_grads(grads)
+        N = args.ND * self.Ninflate
+        ns = [self.nd * np.sqrt(2 * self.momentum_decay / (N * v)) for v in lrs]
+        ckind, m1, m2, ca, cb = (L.COLLECT_NONE, None, None, 1.0, 1.0) if collect is None \
+            else collect
+        K.sgmcmc_step(st, L.SGHMC, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_PHILOX,
+                      one_minus_alpha=1 - self.momentum_decay, prior_sig=self.prior_sig,
+                      sigma2=self.prior_sig ** 2, n_data=N, collect=ckind, mom1=m1, mom2=m2,
+                      collect_a=ca, collect_b=cb, seed=self.seed, chain=self.chain0,
+                      step=self.step_count)
+        self.step_count += 1

@@ -269,7 +269,8 @@ def test_stacked_sgld_trains_and_evaluates():
     assert not S.state.diverged()
 
 
-@pytest.mark.parametrize("cls", ["StackedCSGHMC", "StackedSGLD", "StackedCSGLD"])
+@pytest.mark.parametrize("cls", ["StackedCSGHMC", "StackedSGLD", "StackedCSGLD",
+                                 "StackedSGHMC"])
 def test_stacked_checkpoint_resume_is_exact(cls, tmp_path):
     """Two epochs, save_ckpt, two more epochs == a fresh sampler that loads the
     checkpoint and runs the last two epochs (theta, momentum, moments, bit for
@@ -280,7 +281,7 @@ def test_stacked_checkpoint_resume_is_exact(cls, tmp_path):
     loader = [(xs[i:i + 32].cuda(), ys[i:i + 32].cuda()) for i in range(0, 256, 32)]
     args = _args(epochs=4, nst=2)
     args.momentum = 0.5
-    args.hparams.update({"burnin": 1, "thin": 2})
+    args.hparams.update({"burnin": 1, "thin": 2})  # (momentum_decay: sghmc)
 
     def make():
         torch.manual_seed(11)
@@ -347,6 +348,45 @@ def test_stacked_csgld_trains_and_evaluates():
     nll, err = S.evaluate(loader)
     assert np.isfinite(nll) and err < 0.5
     assert not S.state.diverged()
+
+
+def test_stacked_sghmc_equals_one_chain_launches():
+    """StackedSGHMC: every chain equals one-chain BDL_SGHMC launches with chain
+    id chain0 + k (momentum v, prior theta0, running moments), bit for bit."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd import stacked
+    from bayesdll_amd.flat import FlatState
+    torch.manual_seed(9)
+    K_ = 2
+    args = _args()
+    args.hparams.update({"Ninflate": 10.0, "burnin": 0, "thin": 1, "nst": 2})
+    S = stacked.StackedSGHMC(Net().cuda(), K_, args, chain0=6, init="reinit", net0=Net().cuda())
+    st = S.state
+    segs = [(nm, sh) for nm, sh in zip(st.names, st.shapes)]
+    ones = []
+    for k in range(K_):
+        one = FlatState.from_segments(segs, "head", device="cuda", need_mom=True, need_prior=True,
+                                      init=st.chain_vector(k).clone())
+        one.prior.copy_(st.prior.view(K_, -1)[k, :st.n1])
+        ones.append(one)
+    x = torch.randn(16, 13, device="cuda")
+    y = torch.randint(0, 5, (16,), device="cuda")
+    lrs = (args.lr, args.lr_head)
+    N = args.ND * 10.0
+    for t in range(4):
+        grads, _, _ = S.gradients(x, y)
+        S.update(grads, lrs)
+        for k, one in enumerate(ones):
+            one.use_tensor_grads([grads[nm][k].contiguous().view(-1) for nm in st.names])
+            K.sgmcmc_step(one, L.SGHMC, lrs=lrs,
+                          noise_scale=[np.sqrt(2 * 0.1 / (N * v)) for v in lrs],
+                          noise_mode=L.NOISE_PHILOX, one_minus_alpha=1 - 0.1, prior_sig=1.0,
+                          sigma2=1.0, n_data=N, seed=S.seed, chain=6 + k, step=t)
+    torch.cuda.synchronize()
+    for k, one in enumerate(ones):
+        assert torch.equal(st.theta2d[k, :st.n1], one.theta), k
+        assert torch.equal(st.mom2d[k, :st.n1], one.mom), k
 
 
 def test_stacked_refuses_batchnorm_statistics():
