@@ -20,6 +20,8 @@ Noise modes (`Model.noise_mode`, or env BDL_NOISE_MODE):
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import os
 
 import torch
@@ -30,6 +32,22 @@ from .flat import FlatState
 
 NOISE_MODES = ("philox", "torch", "external")
 MAX_GRAPHS = 4  # captured forward/backward graphs per sampler (one per input shape)
+
+
+@contextlib.contextmanager
+def no_gc():
+    """Keep Python's cyclic GC from running during a HIP-graph capture:
+    torch.cuda.graph collects garbage before capture begins, but an automatic
+    collection triggered by allocations DURING capture can destroy an
+    unrelated object that frees device memory (e.g. an old graph's private
+    pool) — an operation a capturing stream forbids, which aborts the process."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def default_noise_mode():
@@ -263,7 +281,7 @@ class FusedModelBase(nn.Module):
         torch.cuda.set_rng_state(rng, st.device)
         st.zero_grad()  # "tensor" mode: .grad = None, so the graph's gradients are its own
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with no_gc(), torch.cuda.graph(graph):
             if st.grad is not None:  # "flat" mode: the graph zeroes the flat buffer
                 st.grad.zero_()
             out = net(sx)

@@ -44,6 +44,7 @@ from torch.func import functional_call, grad_and_value, vmap
 
 from . import _lib as L
 from . import kernels as K
+from ._base import no_gc
 from ._runner import EVAL_STEP_BASE
 from .cyclical import CyclicalSGMCMC
 from .flat import MAX_TENSOR_RUNS, build_runs, segment_attrs
@@ -262,14 +263,19 @@ class _StackedSampler:
         self.buffers = dict(self.net.named_buffers())
         xdim = 0 if per_chain_batches else None
 
+        # the closures hold the module, not the sampler: no reference cycle,
+        # so a dropped sampler (and its graphs) is freed at once, never by a
+        # later garbage collection
+        net_, bufs_, crit_ = self.net, self.buffers, self.criterion
+
         def loss_fn(tp, fp, x, y):
-            out = functional_call(self.net, ({**tp, **fp}, self.buffers), (x,))
-            return self.criterion(out, y), out
+            out = functional_call(net_, ({**tp, **fp}, bufs_), (x,))
+            return crit_(out, y), out
 
         self._grad = vmap(grad_and_value(loss_fn, has_aux=True),
                           in_dims=(0, 0, xdim, xdim), randomness="different")
         # evaluation: every chain sees the same batch
-        self._fwd = vmap(lambda p, x: functional_call(self.net, (p, self.buffers), (x,)),
+        self._fwd = vmap(lambda p, x: functional_call(net_, (p, bufs_), (x,)),
                          in_dims=(0, None), randomness="different")
 
     def _split(self):
@@ -305,7 +311,7 @@ class _StackedSampler:
                     self._grad(tp, fp, sx, sy)
             torch.cuda.current_stream().wait_stream(side)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            with no_gc(), torch.cuda.graph(graph):
                 grads, (loss, out) = self._grad(tp, fp, sx, sy)
             g = self._graphs[key] = (graph, sx, sy, grads, loss.detach(), out.detach())
         graph, sx, sy, grads, loss, out = g

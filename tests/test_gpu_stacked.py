@@ -389,6 +389,37 @@ def test_stacked_sghmc_equals_one_chain_launches():
         assert torch.equal(st.mom2d[k, :st.n1], one.mom), k
 
 
+def test_graph_capture_with_pending_garbage():
+    """A dropped sampler that owns captured graphs must not be collected in
+    the middle of another capture (freeing a graph's pool on a capturing
+    stream aborts the process): samplers hold no reference cycle, and cyclic
+    GC is off while capturing."""
+    import gc
+    import weakref
+    from bayesdll_amd import stacked
+    x = torch.randn(8, 13, device="cuda")
+    y = torch.randint(0, 5, (8,), device="cuda")
+    old = stacked.StackedCSGHMC(Net().cuda(), 2, _args(), graph=True)
+    old.step(x, y, 0.01)
+    ref = weakref.ref(old)
+    del old
+    assert ref() is None  # freed by reference counting, not left to the GC
+    holder = {"s": stacked.StackedCSGHMC(Net().cuda(), 2, _args(), graph=True)}
+    holder["s"].step(x, y, 0.01)
+    holder["self"] = holder  # an unreachable cycle owning a graph
+    del holder
+    th = gc.get_threshold()
+    gc.set_threshold(1)  # collect at every opportunity
+    try:
+        S = stacked.StackedCSGHMC(Net().cuda(), 3, _args(), graph=True)
+        loss, _ = S.step(x, y, 0.01)
+        torch.cuda.synchronize()
+        assert torch.isfinite(loss).all()
+    finally:
+        gc.set_threshold(*th)
+        gc.collect()
+
+
 def test_stacked_refuses_batchnorm_statistics():
     from bayesdll_amd import stacked
     net = nn.Sequential(nn.Linear(4, 4), nn.BatchNorm1d(4)).cuda()
