@@ -203,3 +203,24 @@ def test_stacked_predictive_averages_over_processes():
     want = probs.mean(0).log()
     for r in range(2):
         torch.testing.assert_close(res[r][2], want, rtol=1e-5, atol=1e-6)
+
+
+def test_no_gc_disables_and_restores_the_collector():
+    import gc
+
+    from bayesdll_amd._base import no_gc
+    assert gc.isenabled()
+    with no_gc():
+        assert not gc.isenabled()
+    assert gc.isenabled()
+    gc.disable()
+    try:
+        with no_gc():
+            pass
+        assert not gc.isenabled()  # left as the caller had it
+    finally:
+        gc.enable()
+    with pytest.raises(RuntimeError):
+        with no_gc():
+            raise RuntimeError("capture failed")
+    assert gc.isenabled()
