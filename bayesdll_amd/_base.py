@@ -36,11 +36,13 @@ MAX_GRAPHS = 4  # captured forward/backward graphs per sampler (one per input sh
 
 @contextlib.contextmanager
 def no_gc():
-    """Keep Python's cyclic GC from running during a HIP-graph capture:
-    torch.cuda.graph collects garbage before capture begins, but an automatic
-    collection triggered by allocations DURING capture can destroy an
-    unrelated object that frees device memory (e.g. an old graph's private
-    pool) — an operation a capturing stream forbids, which aborts the process."""
+    """Keep Python's cyclic GC from running during a HIP-graph capture: an
+    automatic collection triggered by allocations DURING capture can destroy
+    an unrelated object that frees device memory (e.g. an old graph's private
+    pool) — an operation a capturing stream forbids, which aborts the process.
+    (The installed torch.cuda.graph collects garbage before capture only under
+    torch.compiler.config.force_cudagraph_gc; the samplers release their own
+    graphs explicitly, release_graphs, and collect before capturing.)"""
     was = gc.isenabled()
     gc.disable()
     try:
@@ -104,6 +106,8 @@ class FusedModelBase(nn.Module):
         self.div_mode = None
         self.graph = default_graph()
         self._graphs = {}
+        self._graph_bound = None  # the graph whose static gradients the params' .grad hold
+        self.graph_captures = 0   # captures so far (one per input shape, unless released)
         self.overlap = default_overlap()
         self._ovl = None          # per-backward bucket bookkeeping while overlapping
         self._ovl_plan = None
@@ -115,6 +119,7 @@ class FusedModelBase(nn.Module):
     # -------------------------------------------------------------- state
     def state_for(self, net, net0=None):
         if self._state is None or self._state_net is not net:
+            self.release_graphs()  # graphs captured against the old state's buffers
             if self.noise_mode not in NOISE_MODES:
                 raise ValueError(f"noise_mode must be one of {NOISE_MODES}")
             self._state = FlatState(net, net0, readout_name=getattr(net, "readout_name", None),
@@ -238,7 +243,8 @@ class FusedModelBase(nn.Module):
         get a gradient is fixed at capture (the eager path re-checks it every
         step, like the reference's `if p.grad is not None`).  One graph per
         (input shape, dtype, train mode, criterion), at most MAX_GRAPHS;
-        beyond that, or when the gradient views were re-bound, eager."""
+        beyond that, eager.  A replay binds every .grad to its graph's static
+        gradients, so switching between shapes never recaptures."""
         key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, net.training, id(criterion),
                id(net))
         g = self._graphs.get(key)
@@ -250,9 +256,15 @@ class FusedModelBase(nn.Module):
                 self.graph = False
                 return None
             self._graphs[key] = g
-        if any(p.grad is not gt for p, gt in zip(st.params, g["grads"])):
-            self._graphs.clear()    # user code re-bound .grad: recapture on the next step
-            return None
+        if g is not self._graph_bound or any(p.grad is not gt
+                                             for p, gt in zip(st.params, g["grads"])):
+            # another shape's graph (a ragged last batch, then the next epoch's
+            # full one), an eager step or user code left other tensors in .grad:
+            # point every .grad at this graph's static gradient outputs (the
+            # update reads them through the graph's table either way)
+            for p, gt in zip(st.params, g["grads"]):
+                p.grad = gt
+        self._graph_bound = g
         g["x"].copy_(x)
         g["y"].copy_(y)
         g["graph"].replay()
@@ -261,8 +273,21 @@ class FusedModelBase(nn.Module):
             st._touched[:] = g["touched"]
         return g["loss"], g["out"].detach().clone()
 
+    def release_graphs(self):
+        """Drop every captured graph (and with it its private memory pool) now,
+        deterministically, on the caller's stream — never from a garbage
+        collection that might run inside another capture.  Called when the
+        sampler state is rebuilt (its buffers are what the graphs captured);
+        call it when done with a sampler instead of leaving the graphs to the
+        garbage collector."""
+        graphs, self._graphs, self._graph_bound = self._graphs, {}, None
+        if graphs:
+            torch.cuda.synchronize()  # no replay of these graphs still in flight
+        graphs.clear()
+
     def _capture(self, st, net, x, y, criterion):
         sx, sy = x.detach().clone(), y.detach().clone()
+        gc.collect()  # pending garbage (old pools included) goes before the capture, not in it
         # warm-up passes on a side stream (library handles, autotuned kernels)
         # must not move the network's state: keep buffers (BatchNorm running
         # statistics) and the device RNG as they were
@@ -296,6 +321,7 @@ class FusedModelBase(nn.Module):
         # AccumulateGrad nodes would otherwise outlive the capture and meet the
         # next capture's warm-up on another stream
         out, loss = out.detach(), loss.detach()
+        self.graph_captures += 1
         return {"graph": graph, "x": sx, "y": sy, "out": out, "loss": loss,
                 "grads": [p.grad for p in st.params], "touched": list(st._touched),
                 "table": st.grad_table()}

@@ -6,12 +6,15 @@ communication: each rank owns a full chain (theta, v, moments resident in its
 own HBM) keyed by its rank (Philox chain id; seed = base + rank).
 
 The only exchange is at evaluation: the posterior-predictive average over
-chains.  Per batch, each rank holds log p_k(y|x) ([B, C], already averaged over
-its own nst draws as logsumexp(...) - log(nst), methods/sgld.py:300); the
-ensemble predictive is log((1/K) sum_k p_k), one all_reduce(SUM) of
-probabilities over RCCL (backend "nccl" on ROCm; "gloo" on CPU for tests).
-Messages are B x C fp32 (512 KB at B=128, C=1000): latency-bound, far below
-one xGMI link, so no bucketing is needed.
+chains.  Per batch, each rank holds its chain's predictive scores ([B, C]: the
+log-mean-exp over its own nst draws, methods/sgld.py:300, or the csghmc
+mixture's weighted scores, methods/csghmc.py:470-480, which the reference
+feeds to the loss as logits); the ensemble predictive is
+log((1/K) sum_k softmax(s_k)), computed stably as a log-mean-exp over ranks:
+all_reduce(MAX) of log_softmax(s_k) for the shift, then all_reduce(SUM) of
+exp(log_softmax(s_k) - max) over RCCL (backend "nccl" on ROCm; "gloo" on CPU
+for tests).  Messages are B x C fp32 (512 KB at B=128, C=1000): latency-bound,
+far below one xGMI link, so no bucketing is needed.
 """
 from __future__ import annotations
 
@@ -50,16 +53,20 @@ def init_chains(backend=None):
     return rank(), world(), device
 
 
-def _all_reduce_sum(t):
-    """all_reduce(SUM) in place.  gloo (CPU tests, ranks sharing one GPU) is
-    fed a host copy of a device tensor; RCCL ("nccl") reduces on the device."""
+def _all_reduce(t, op=dist.ReduceOp.SUM):
+    """all_reduce in place.  gloo (CPU tests, ranks sharing one GPU) is fed a
+    host copy of a device tensor; RCCL ("nccl") reduces on the device."""
     if t.is_cuda and dist.get_backend() == "gloo":
         h = t.cpu()
-        dist.all_reduce(h, op=dist.ReduceOp.SUM)
+        dist.all_reduce(h, op=op)
         t.copy_(h)
     else:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dist.all_reduce(t, op=op)
     return t
+
+
+def _all_reduce_sum(t):
+    return _all_reduce(t, dist.ReduceOp.SUM)
 
 
 def chain_seed(base_seed):
@@ -67,13 +74,21 @@ def chain_seed(base_seed):
     return int(base_seed) + rank()
 
 
-def average_predictive(logp):
-    """log((1/K) sum_k exp(logp_k)) over the K chains (one all_reduce)."""
+def average_predictive(scores):
+    """Ensemble predictive over the K chains: log((1/K) sum_k softmax(s_k)),
+    per class.  Each chain's scores are normalised first (log_softmax: the
+    csghmc mixture's weighted logits are not log-probabilities, and chains may
+    differ in logit scale), then a max-shifted log-mean-exp over ranks — no
+    overflow for large logits, no -inf for classes every chain finds unlikely.
+    One process: the scores are returned unchanged (the reference's
+    single-chain evaluation)."""
     k = world()
     if k == 1:
-        return logp
-    p = _all_reduce_sum(logp.float().exp())
-    return (p / k).log()
+        return scores
+    lp = torch.log_softmax(scores.float(), dim=1)
+    shift = _all_reduce(lp.clone(), dist.ReduceOp.MAX)
+    s = _all_reduce_sum((lp - shift).exp())
+    return shift + (s / k).log()
 
 
 def gather_logits(logits_all):

@@ -73,87 +73,120 @@ def build_runs(offsets, numels, attrs, n):
 PLACEMENT_MIN_ELEMS = 1 << 24  # below ~64 MB per vector placement effects are noise
 
 
-def placed_vectors(n, device, names, method, candidates=None):
-    """Allocate the chain's swept fp32 vectors (`names` among theta, grad, mom,
-    prior) so that the sweep runs fast where they land physically.
+PLACEMENT_FAST = 0.97   # a pair is "cross-class" if its sweep is <= 97 % of the slowest seen
+PLACEMENT_MAX_EXTRA = 3  # at most this many spare vectors are allocated while pairing
 
-    The sweep time of the same kernel depends on where its vectors' pages land
-    (HBM channel / bank interplay between the concurrently streamed vectors):
-    on one MI355X six fresh (theta, grad, mom) allocations ran the ViT-L/32
-    explore sweep in 0.967-1.051 ms, each set stable to 0.2 % across passes
-    (profiles/round1/placement_probe.log).  So: allocate `candidates` sets,
-    time `method`'s production kernel on each (scratch contents, 8 launches),
-    keep the fastest set, free the rest.  Results never depend on placement.
 
-    The times are bimodal (a fast cluster ~0.97-0.99 ms and a slow one
-    ~1.04-1.10 ms on ViT-L/32) and a process can draw six slow sets in a row
-    (profiles/round1/bench_long.jsonl), so candidates come in rounds of
-    `candidates`: after a round, stop if the best is clearly in a faster
-    cluster (<= 96.5 % of the median) or all are alike (spread < 2 %), else
-    draw another round (earlier sets stay allocated, so the new ones land on
-    other pages), up to BDL_PLACEMENT_MAX sets (18) within a quarter of the
-    free HBM.  Returns ({name: tensor}, info)."""
-    import os
-    k = int(os.environ.get("BDL_PLACEMENT_CANDIDATES", "6")) if candidates is None else candidates
-    kmax = max(k, int(os.environ.get("BDL_PLACEMENT_MAX", "18"))) if candidates is None else k
-    f32 = dict(dtype=torch.float32, device=device)
-    if method is not None and k > 1 and n >= PLACEMENT_MIN_ELEMS:
-        # the candidates live at the same time: keep them within a quarter of
-        # the free HBM
-        free, _ = torch.cuda.mem_get_info(device)
-        cap = int(0.25 * free // (len(names) * n * 4))
-        k, kmax = min(k, cap), min(kmax, cap)
-    if method is None or k <= 1 or n < PLACEMENT_MIN_ELEMS:
-        return {nm: torch.empty(n, **f32) for nm in names}, None
+def _placement_launcher(method, vs, n, device, runs):
+    """The sampler's production kernel on scratch vectors `vs` (role -> tensor)."""
     from types import SimpleNamespace
 
     from . import kernels as K
+    st = SimpleNamespace(theta=vs["theta"], grad=vs["grad"], mom=vs.get("mom"),
+                         prior=vs.get("prior"), noise=None, runs=runs, nruns=1, n=n,
+                         device=device)
+    if method == "adam" and "adam_m" in vs:
+        return lambda: K.adam_step(
+            st, L.ADAM_SGHMC, adam_m=vs["adam_m"], adam_v=vs["adam_v"],
+            sgd_buf=vs.get("sgd_buf"), beta1=0.9, beta2=0.999, eps=1e-8, t=3,
+            momentum_decay=0.1, nd=0.01, lrs=(1e-4, 1e-4), noise_mode=L.NOISE_PHILOX,
+            sigma2=1.0, n_data=1e6, mu=0.5, momentum="sgd_buf" in vs)
+    if method == "csghmc":
+        return lambda: K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-4, 1e-4), noise_scale=(0.0, 0.0),
+                                     noise_mode=L.NOISE_NONE, one_minus_alpha=0.9, prior_sig=1.0)
+    if method in ("sgld", "adam"):
+        return lambda: K.sgmcmc_step(st, L.SGLD, lrs=(1e-4, 1e-4), noise_scale=(1e-3, 1e-3),
+                                     noise_mode=L.NOISE_PHILOX, sigma2=1.0, n_data=1e6, mu=0.5,
+                                     momentum=st.mom is not None)
+    raise ValueError(f"placed_vectors: unknown method {method!r}")
+
+
+def _time_launch(launch, device, reps=5):
+    launch()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for e0, e1 in ev:
+        e0.record()
+        launch()
+        e1.record()
+    torch.cuda.synchronize(device)
+    return float(np.median([a.elapsed_time(b) for a, b in ev]))
+
+
+def placed_vectors(n, device, names, method, max_extra=None):
+    """Allocate the chain's swept fp32 vectors (`names` among theta, grad, mom,
+    prior, extra state) and choose WHICH allocation plays which role so that
+    the two vectors the step rewrites in place — theta and mom — sit in
+    different physical placement classes.
+
+    What was measured (profiles/round2/placement/, tools/placement_probe2.cpp,
+    the production explore kernel on ViT-L/32-sized vectors): the sweep is
+    bimodal, 0.955-0.97 ms or 1.04-1.10 ms, and which one is decided by ONE
+    thing — whether theta and mom (the two read-modify-write streams) are in
+    the same placement class.  Every ordered (theta, grad, mom) triple of 9
+    allocations (role_mix/): fast iff class(theta) != class(mom); the
+    read-only gradient's class never matters.  The class is a property of the
+    physical memory an allocation lands on, invisible from user space: moving
+    mom by 256 B ... 1 GB inside its allocation never changes it
+    (mom_offset_*), physically contiguous allocations and VMM-mapped 2 MB /
+    1 GB chunks are as bimodal as hipMalloc (allocators/), and classes come in
+    long runs in allocation order (class_map/), which is why consecutive
+    allocations so often pair badly.
+
+    So the choice is a role assignment, not a lottery over fresh sets: the
+    vectors are allocated once; for every unordered pair of allocations the
+    method's kernel is timed with that pair as (theta, mom) and the others in
+    the remaining roles (5 launches each, scratch contents); a pair at <= 97 %
+    of the slowest is cross-class and is taken.  Only when every pair is alike
+    (all allocations in one class) is one spare vector allocated and paired,
+    up to PLACEMENT_MAX_EXTRA; spares not chosen are freed.  Results never
+    depend on placement.  Returns ({name: tensor}, info) with the timing of
+    the allocation-order assignment ("default_ms") next to the chosen one."""
+    import itertools
+    import os
+    f32 = dict(dtype=torch.float32, device=device)
+    vecs = [torch.zeros(n, **f32) for _ in names]
+    if method is None or n < PLACEMENT_MIN_ELEMS or "mom" not in names or "theta" not in names:
+        return dict(zip(names, vecs)), None
+    if max_extra is None:
+        max_extra = int(os.environ.get("BDL_PLACEMENT_MAX_EXTRA", str(PLACEMENT_MAX_EXTRA)))
+    free, _ = torch.cuda.mem_get_info(device)
+    max_extra = max(0, min(max_extra, int(0.25 * free // (n * 4))))
     runs = build_runs([0], [n], [L.ATTR_PRIOR], n).to(device)
-    times, sets = [], []
+    it, im = names.index("theta"), names.index("mom")
+    others = [i for i in range(len(names)) if i not in (it, im)]
+
+    def assign(a, b):
+        """theta = vecs[a], mom = vecs[b], the other roles in allocation order."""
+        rest = [j for j in range(len(vecs)) if j not in (a, b)]
+        roles = {"theta": vecs[a], "mom": vecs[b]}
+        for i, j in zip(others, rest):
+            roles[names[i]] = vecs[j]
+        return roles
+
+    times = {}
+    default = (it, im)
+    times[default] = _time_launch(_placement_launcher(method, assign(*default), n, device, runs),
+                                  device)
+    extra = 0
     while True:
-        if len(times) >= k and len(times) % k == 0:
-            med, best_t = float(np.median(times)), min(times)
-            if (best_t <= 0.965 * med or max(times) <= 1.02 * best_t
-                    or len(times) + k > kmax):
-                break
-        vs = {nm: torch.zeros(n, **f32) for nm in names}
-        st = SimpleNamespace(theta=vs["theta"], grad=vs["grad"], mom=vs.get("mom"),
-                             prior=vs.get("prior"), noise=None, runs=runs, nruns=1, n=n,
-                             device=device)
-        if method == "adam" and "adam_m" in vs:
-            def launch():
-                K.adam_step(st, L.ADAM_SGHMC, adam_m=vs["adam_m"], adam_v=vs["adam_v"],
-                            sgd_buf=vs.get("sgd_buf"), beta1=0.9, beta2=0.999, eps=1e-8, t=3,
-                            momentum_decay=0.1, nd=0.01, lrs=(1e-4, 1e-4),
-                            noise_mode=L.NOISE_PHILOX, sigma2=1.0, n_data=1e6, mu=0.5,
-                            momentum="sgd_buf" in vs)
-        elif method == "csghmc":
-            def launch():
-                K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-4, 1e-4), noise_scale=(0.0, 0.0),
-                              noise_mode=L.NOISE_NONE, one_minus_alpha=0.9, prior_sig=1.0)
-        elif method in ("sgld", "adam"):
-            def launch():
-                K.sgmcmc_step(st, L.SGLD, lrs=(1e-4, 1e-4), noise_scale=(1e-3, 1e-3),
-                              noise_mode=L.NOISE_PHILOX, sigma2=1.0, n_data=1e6, mu=0.5,
-                              momentum=st.mom is not None)
-        else:
-            raise ValueError(f"placed_vectors: unknown method {method!r}")
-        for _ in range(2):
-            launch()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(8)]
-        for e0, e1 in ev:
-            e0.record()
-            launch()
-            e1.record()
-        torch.cuda.synchronize(device)
-        times.append(float(np.median([a.elapsed_time(b) for a, b in ev])))
-        sets.append(vs)
-    best = int(np.argmin(times))
-    chosen = sets[best]
-    del sets  # the other candidates' blocks stay in torch's cache for later allocations
-    return chosen, {"candidates_ms": [round(t, 4) for t in times], "chosen": best,
-                    "method": method}
+        for a, b in itertools.combinations(range(len(vecs)), 2):
+            if (a, b) not in times and (b, a) not in times:
+                times[(a, b)] = _time_launch(
+                    _placement_launcher(method, assign(a, b), n, device, runs), device)
+        best = min(times, key=times.get)
+        if times[best] <= PLACEMENT_FAST * max(times.values()) or extra >= max_extra:
+            break
+        vecs.append(torch.zeros(n, **f32))  # all alike so far: one more allocation
+        extra += 1
+    chosen = assign(*best)
+    out = {nm: chosen[nm] for nm in names}
+    keep = {id(t) for t in out.values()}
+    spare = [t for t in vecs if id(t) not in keep]
+    del vecs, chosen, spare  # unchosen spares return to torch's cache
+    return out, {"default_ms": round(times[default], 4), "chosen_ms": round(times[best], 4),
+                 "pairs_timed": len(times), "spares": extra, "method": method,
+                 "pairs_ms": sorted(round(t, 4) for t in times.values())}
 
 
 GRAD_MODES = ("tensor", "flat")

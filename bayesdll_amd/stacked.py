@@ -302,6 +302,8 @@ class _StackedSampler:
         key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype)
         g = self._graphs.get(key)
         if g is None:
+            import gc
+            gc.collect()  # pending garbage (old graphs' pools) goes before the capture
             tp, fp = self._split()
             sx, sy = x.clone(), y.clone()
             side = torch.cuda.Stream(device=self.state.device)
@@ -319,6 +321,14 @@ class _StackedSampler:
         sy.copy_(y)
         graph.replay()
         return grads, loss, out
+
+    def release_graphs(self):
+        """Drop the captured graphs (and their memory pools) now, after the
+        device has finished with them — not whenever a collection happens."""
+        graphs, self._graphs = self._graphs, {}
+        if graphs:
+            torch.cuda.synchronize(self.state.device)
+        graphs.clear()
 
     def step(self, x, y, *a, **kw):
         """One step of all K chains: vmapped forward/backward, then one fused

@@ -9,9 +9,11 @@ the posterior moments on thinned sample steps — all in the fused HIP kernel.
 Gradients are a synthetic resident buffer (g ~ N(0, 1e-3^2)), re-read every
 step; theta ~ N(0, 0.02^2), v = 0 at step 0.
 
-Multi-GPU (`torch.distributed.run --nproc-per-node N`): one independent chain
-per GPU (seed 42 + rank, Philox chain id = rank); no collective inside the
-timed region; value = total chain-steps / max-over-ranks wall time.
+Multi-GPU (`python bench.py --gpus N` starts N rank processes itself;
+under `torch.distributed.run --nproc-per-node N` the launcher's ranks are
+used, and WORLD_SIZE must equal --gpus): one independent chain per GPU
+(seed 42 + rank, Philox chain id = rank); no collective inside the timed
+region; value = total chain-steps / max-over-ranks wall time.
 
 Prints one JSON line (rank 0).  Extra fields: hbm_gbs (algorithmic), the
 per-kernel-kind table with HIP-event timings, roofline of the dominant
@@ -121,10 +123,56 @@ class LaunchTimer:
         return per
 
 
-def dist_setup():
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` without an outside launcher: start N rank
+    processes of this same command (RANK / LOCAL_RANK / WORLD_SIZE, rendezvous
+    on 127.0.0.1), one per GPU, before this process touches the GPU; wait for
+    all of them and return the first non-zero exit status (the others are
+    stopped), else 0.  Rank 0 prints the JSON line."""
+    import signal
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:  # one rank failed: the barrier would never complete
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
+def dist_setup(expected):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != expected:
+        # a line whose n_gpus differs from --gpus would be mislabelled
+        sys.stderr.write(f"bench.py: --gpus {expected} but WORLD_SIZE={world}\n")
+        sys.exit(2)
     if world > 1:
         import torch.distributed as dist
         backend = os.environ.get("BDL_BENCH_BACKEND", "nccl")  # nccl == RCCL on ROCm
@@ -246,7 +294,9 @@ def e2e_steps(steps, warmup, local, seed, graph=False):
 
 def main():
     a = parse()
-    dist, rank, world, local = dist_setup()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a.gpus))
+    dist, rank, world, local = dist_setup(a.gpus)
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
     from bayesdll_amd.cyclical import CyclicalSGMCMC
@@ -493,6 +543,10 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                      "traffic": traffic,
+                     # not this run's counters: rocprofv3 PMC (FETCH/WRITE_SIZE passes) of the
+                     # same kernel on the same workload, per launch, committed under profiles/
+                     "traffic_source": (f"{os.path.relpath(a.traffic, ROOT)}[{a.backbone}][{dominant}]"
+                                        if traffic is not None else None),
                      "alg_bytes_per_launch": alg_bytes},
     }
     if not a.no_aux:

@@ -51,6 +51,8 @@ int main(void) {
   P(bdl_step_args, noise_scale) P(bdl_step_args, mu) P(bdl_step_args, collect_b)
   P(bdl_step_args, seed) P(bdl_step_args, step) P(bdl_moments_args, collect_a)
   P(bdl_sample_args, ratio) P(bdl_sample_args, step) P(bdl_run, attr) P(bdl_segment, attr)
+  P(bdl_step_args, grad_base) P(bdl_step_args, nonfinite) P(bdl_step_args, philox_offset)
+  P(bdl_step_args, chain_groups) P(bdl_step_args, inv_collect_b) P(bdl_sample_args, chain_groups)
   return 0;
 }
 """
@@ -431,3 +433,45 @@ def test_tools_and_examples_compile():
     for f in files:
         with open(f) as fh:
             compile(fh.read(), f, "exec")
+
+
+def _reference_binding():
+    import importlib.util
+    path = os.path.join(ROOT, "examples", "reference_binding.py")
+    spec = importlib.util.spec_from_file_location("reference_binding", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod, path
+
+
+def test_integration_snippet_is_the_tested_reference_binding():
+    """INTEGRATION.md §3 shows examples/reference_binding.py verbatim, so the
+    documented binding is the one these tests check."""
+    _, path = _reference_binding()
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert open(path).read() in doc
+    assert "ABI version 6" in doc and "ABI version 5" not in doc
+
+
+def test_reference_binding_struct_matches_header_and_library():
+    """The maintainer's ctypes StepArgs has the v6 header's size and every
+    field at the header's offset (so the library never reads past it), and
+    load() accepts the shipped library and refuses another ABI version."""
+    from bayesdll_amd import _lib as L
+    rb, _ = _reference_binding()
+    lay = {k: int(v) for k, v in _c_layout().items()}
+    assert C.sizeof(rb.StepArgs) == lay["bdl_step_args"] == C.sizeof(L.StepArgs)
+    assert C.sizeof(rb.Run) == lay["bdl_run"] and C.sizeof(rb.Segment) == lay["bdl_segment"]
+    assert [f for f, _ in rb.StepArgs._fields_] == [f for f, _ in L.StepArgs._fields_]
+    for f, _ in L.StepArgs._fields_:
+        assert getattr(rb.StepArgs, f).offset == getattr(L.StepArgs, f).offset, f
+    for key, v in lay.items():
+        if key.startswith("bdl_step_args."):
+            assert getattr(rb.StepArgs, key.split(".")[1]).offset == v, key
+    lib = rb.load(L.LIB_PATH)
+    assert lib.bdl_version() == rb.ABI_VERSION == L.ABI_VERSION
+    runs, nr = rb.run_table(lib, [("enc.weight", 10), ("enc.bias", 3), ("head.weight", 5)], "head")
+    assert [(runs[i].end, runs[i].attr) for i in range(nr)] == [(13, 2), (18, 3)]
+    rb.ABI_VERSION = L.ABI_VERSION - 1
+    with pytest.raises(RuntimeError, match="ABI"):
+        rb.load(L.LIB_PATH)

@@ -3,6 +3,7 @@
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -32,8 +33,17 @@ def _worker(r, world, port, q):
         gathered = chains.gather_logits(la)
         m1, m2 = torch.randn(1000, generator=g), torch.rand(1000, generator=g)
         p1, p2 = chains.pool_moments(m1, m2, count=r + 1)
-        q.put((r, logp, avg, la, gathered, default_chain(), chains.chain_seed(42),
-               (m1, m2, p1, p2)))
+        # nst = 0 mixture scores: weighted raw logits of a large scale (exp overflows
+        # fp32 above ~88; every chain puts a class below exp's underflow)
+        big = torch.randn(8, 5, generator=g) * 300.0
+        big[:, 4] = -5000.0
+        avg_big = chains.average_predictive(big)
+        # plain numpy over the queue: a torch tensor would travel as a shared-memory
+        # fd the parent may open only after this worker has exited
+        np_ = lambda t: t.numpy().copy()
+        q.put((r, np_(logp), np_(avg), np_(la), np_(gathered), default_chain(),
+               chains.chain_seed(42), tuple(np_(t) for t in (m1, m2, p1, p2)),
+               (np_(big), np_(avg_big))))
     finally:
         dist.destroy_process_group()
 
@@ -48,8 +58,10 @@ def test_average_predictive_and_gather_chains(world):
         p.start()
     res = {}
     for _ in range(world):
-        r, logp, avg, la, gathered, chain, seed, mom = q.get(timeout=120)
-        res[r] = (logp, avg, la, gathered, chain, seed, mom)
+        r, logp, avg, la, gathered, chain, seed, mom, big = q.get(timeout=120)
+        t = torch.from_numpy
+        res[r] = (t(logp), t(avg), t(la), t(gathered), chain, seed, tuple(t(m) for m in mom),
+                  (t(big[0]), t(big[1])))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -68,6 +80,13 @@ def test_average_predictive_and_gather_chains(world):
         torch.testing.assert_close(res[r][6][3].double(), want2, rtol=1e-6, atol=1e-6)
     # the averaged predictive is a proper distribution
     torch.testing.assert_close(want.exp().sum(1), torch.ones(8))
+    # large / very negative scores: finite, and equal to the float64 log-mean of softmaxes
+    want_big = torch.logsumexp(torch.stack(
+        [torch.log_softmax(res[r][7][0].double(), 1) for r in range(world)]), 0) - np.log(world)
+    for r in range(world):
+        got = res[r][7][1]
+        assert torch.isfinite(got).all()
+        torch.testing.assert_close(got.double(), want_big, rtol=1e-5, atol=1e-4)
 
 
 def test_single_process_is_identity():

@@ -31,12 +31,23 @@ def _free_port():
     return port
 
 
-def test_bench_two_ranks_gloo():
-    env = dict(os.environ, BDL_BENCH_BACKEND="gloo", BDL_PLACEMENT_CANDIDATES="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5",
-           "--backbone", "resnet101", "--no-autotune", "--e2e-steps", "0"]
+BENCH_ARGS = ["--gpus", "2", "--steps", "20", "--warmup", "5", "--backbone", "resnet101",
+              "--no-autotune", "--e2e-steps", "0", "--no-placement"]
+
+
+@pytest.mark.parametrize("launcher", ["torchrun", "self"])
+def test_bench_two_ranks_gloo(launcher):
+    """Under torch.distributed.run, and as `python bench.py --gpus 2` with no
+    outside launcher (bench.py starts its own ranks): the same one line."""
+    env = dict(os.environ, BDL_BENCH_BACKEND="gloo")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    bench = os.path.join(ROOT, "bench.py")
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", bench] + BENCH_ARGS
+    else:
+        cmd = [sys.executable, bench] + BENCH_ARGS
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, (p.stdout + p.stderr)[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

@@ -8,7 +8,7 @@ Checks, for cSGHMC and SGLD:
     during sampling, bit for bit;
   * the chains differ (chain id separates the noise streams);
   * Runner.evaluate's predictive is the cross-chain posterior-predictive
-    average log((1/K) sum_k exp(logp_k)) of the chains' own predictives, and
+    average log((1/K) sum_k softmax(s_k)) of the chains' own predictive scores, and
     every rank holds the same one; per-chain logits_all stay per chain.
 """
 import os
@@ -79,8 +79,9 @@ def test_two_chain_ensemble_matches_single_chains(method, tmp_path):
         np.testing.assert_array_equal(ranks[r]["logits_all"], singles[r]["logits_all"])
         np.testing.assert_array_equal(ranks[r]["targets"], singles[0]["targets"])
     assert not np.array_equal(singles[0]["theta"], singles[1]["theta"])
-    # ensemble predictive = log-mean-exp over the chains' own predictives
+    # ensemble predictive = log-mean-exp over the chains' own (normalised) predictives
     lp = np.stack([s["logits"].astype(np.float64) for s in singles])
+    lp = lp - np.log(np.exp(lp).sum(axis=2, keepdims=True))  # log_softmax per chain
     want = np.log(np.mean(np.exp(lp), axis=0))
     for r in range(WORLD):
         np.testing.assert_allclose(ranks[r]["logits"], want, rtol=0, atol=2e-6)

@@ -580,8 +580,9 @@ def test_full_size_vit_sghmc_matches_torch():
 
 
 def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
-    """flat.placed_vectors: candidate sets are timed and the fastest kept; the
-    update itself never depends on where the vectors live."""
+    """flat.placed_vectors: every (theta, mom) pairing of the allocations is
+    timed and the fastest kept; the update itself never depends on where the
+    vectors live."""
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
     from bayesdll_amd.flat import FlatState, PLACEMENT_MIN_ELEMS
@@ -593,8 +594,12 @@ def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
             assert st.placement_info is None
         else:
             info = st.placement_info
-            assert len(info["candidates_ms"]) >= 2
-            assert info["candidates_ms"][info["chosen"]] == min(info["candidates_ms"])
+            assert info["pairs_timed"] >= 3  # theta, grad, mom: three pairings at least
+            assert info["chosen_ms"] == min(info["pairs_ms"])
+            assert info["chosen_ms"] <= info["default_ms"]
+            assert 0 <= info["spares"] <= 3
+            ptrs = {st.theta.data_ptr(), st.grad.data_ptr(), st.mom.data_ptr()}
+            assert len(ptrs) == 3
         g = torch.Generator(device=DEV).manual_seed(0)
         st.theta.normal_(0, 0.02, generator=g)
         st.grad.normal_(0, 1e-3, generator=g)

@@ -517,8 +517,8 @@ def test_reference_written_checkpoint_loads_and_predicts_alike(method):
 def test_graph_mode_is_bit_identical_to_eager(method):
     """Model.graph (BDL_GRAPH=1): forward + backward replayed from a captured
     HIP graph gives the eager chain bit for bit (same kernels, same order),
-    including a ragged last batch (a second graph) and the loss values the
-    Runner logs."""
+    including a ragged last batch (a second graph, captured once for all
+    epochs) and the loss values the Runner logs."""
     import bayesdll_amd.csghmc as csghmc
     import bayesdll_amd.sgld as sgld
     from bayesdll_amd.sgld import FusedSGD
@@ -556,6 +556,9 @@ def test_graph_mode_is_bit_identical_to_eager(method):
     m_e, th_e, lo_e, out_e = run(False)
     m_g, th_g, lo_g, out_g = run(True)
     assert len(m_g._graphs) == 2 and not m_e._graphs
+    # 3 epochs of (64, 64, 64, 8): one capture per shape, none again when the
+    # next epoch's full batch follows the ragged one
+    assert m_g.graph_captures == 2
     assert lo_g == lo_e
     for a, b in zip(out_g, out_e):
         assert torch.equal(a, b)

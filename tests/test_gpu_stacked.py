@@ -392,10 +392,16 @@ def test_stacked_sghmc_equals_one_chain_launches():
 def test_graph_capture_with_pending_garbage():
     """A dropped sampler that owns captured graphs must not be collected in
     the middle of another capture (freeing a graph's pool on a capturing
-    stream aborts the process): samplers hold no reference cycle, and cyclic
-    GC is off while capturing."""
+    stream aborts the process).  The invariant itself is checked: a gc
+    callback fails the test if a collection ever starts while the current
+    stream is capturing, with an unreachable graph-owning cycle created just
+    before each capture and the collector at its most eager threshold.
+    Samplers hold no reference cycle; capture collects pending garbage first
+    and keeps the cyclic GC off until the capture ends; release_graphs()
+    frees graphs deterministically."""
     import gc
     import weakref
+    import bayesdll_amd.csghmc as csghmc
     from bayesdll_amd import stacked
     x = torch.randn(8, 13, device="cuda")
     y = torch.randint(0, 5, (8,), device="cuda")
@@ -404,20 +410,41 @@ def test_graph_capture_with_pending_garbage():
     ref = weakref.ref(old)
     del old
     assert ref() is None  # freed by reference counting, not left to the GC
-    holder = {"s": stacked.StackedCSGHMC(Net().cuda(), 2, _args(), graph=True)}
-    holder["s"].step(x, y, 0.01)
-    holder["self"] = holder  # an unreachable cycle owning a graph
-    del holder
+    during_capture = []
+
+    def watch(phase, info):
+        if phase == "start" and torch.cuda.is_current_stream_capturing():
+            during_capture.append(info)
+
+    def garbage_cycle():
+        holder = {"s": stacked.StackedCSGHMC(Net().cuda(), 2, _args(), graph=True)}
+        holder["s"].step(x, y, 0.01)
+        holder["self"] = holder  # unreachable cycle owning a captured graph
     th = gc.get_threshold()
+    gc.callbacks.append(watch)
     gc.set_threshold(1)  # collect at every opportunity
     try:
+        garbage_cycle()
         S = stacked.StackedCSGHMC(Net().cuda(), 3, _args(), graph=True)
         loss, _ = S.step(x, y, 0.01)
+        # the Model path: two input shapes, a cycle created before each capture
+        net = Net().cuda()
+        model = csghmc.Model(100.0, prior_sig=1.0, momentum_decay=0.1)
+        model.graph = True
+        for xb, yb in ((x, y), (x[:5], y[:5])):
+            garbage_cycle()
+            model(xb, yb, net, None, torch.nn.CrossEntropyLoss(), [1e-3, 1e-3], 1.0, 1.0)
+        assert model.graph_captures == 2
+        model.release_graphs()
+        S.release_graphs()
+        assert not model._graphs and not S._graphs
         torch.cuda.synchronize()
         assert torch.isfinite(loss).all()
     finally:
+        gc.callbacks.remove(watch)
         gc.set_threshold(*th)
         gc.collect()
+    assert not during_capture, during_capture
 
 
 def test_stacked_refuses_batchnorm_statistics():
