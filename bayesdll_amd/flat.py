@@ -73,8 +73,9 @@ def build_runs(offsets, numels, attrs, n):
 PLACEMENT_MIN_ELEMS = 1 << 24  # below ~64 MB per vector placement effects are noise
 
 
-PLACEMENT_FAST = 0.97   # a pair is "cross-class" if its sweep is <= 97 % of the slowest seen
-PLACEMENT_MAX_EXTRA = 3  # at most this many spare vectors are allocated while pairing
+PLACEMENT_GAP = 1.04      # two placement classes seen: a gap of >= 4 % in the sorted pair times
+PLACEMENT_MAX_EXTRA = 4   # at most this many spare vectors are allocated while pairing
+PLACEMENT_SKIP0 = 2 << 30  # first spacer allocated ahead of a spare (doubles each round)
 
 
 def _placement_launcher(method, vs, n, device, runs):
@@ -113,6 +114,13 @@ def _time_launch(launch, device, reps=5):
     return float(np.median([a.elapsed_time(b) for a, b in ev]))
 
 
+def _two_classes(times):
+    """Do the timed (theta, mom) pairings fall into a fast and a slow cluster?
+    (The clusters are 6-10 % apart; pairs inside one class spread by <= 3 %.)"""
+    t = sorted(times)
+    return any(b > PLACEMENT_GAP * a for a, b in zip(t, t[1:]))
+
+
 def placed_vectors(n, device, names, method, max_extra=None):
     """Allocate the chain's swept fp32 vectors (`names` among theta, grad, mom,
     prior, extra state) and choose WHICH allocation plays which role so that
@@ -128,20 +136,24 @@ def placed_vectors(n, device, names, method, max_extra=None):
     read-only gradient's class never matters.  The class is a property of the
     physical memory an allocation lands on, invisible from user space: moving
     mom by 256 B ... 1 GB inside its allocation never changes it
-    (mom_offset_*), physically contiguous allocations and VMM-mapped 2 MB /
-    1 GB chunks are as bimodal as hipMalloc (allocators/), and classes come in
-    long runs in allocation order (class_map/), which is why consecutive
-    allocations so often pair badly.
+    (mom_offset_*), physically contiguous allocations and VMM-mapped 1 GB
+    chunks are as bimodal as hipMalloc (VMM 2 MB chunks land in between: a mix
+    of classes along the vector; allocators/), and the classes come
+    in runs of several GB in allocation order (class_map/) — which is why
+    consecutive allocations so often pair badly.
 
     So the choice is a role assignment, not a lottery over fresh sets: the
     vectors are allocated once; for every unordered pair of allocations the
     method's kernel is timed with that pair as (theta, mom) and the others in
-    the remaining roles (5 launches each, scratch contents); a pair at <= 97 %
-    of the slowest is cross-class and is taken.  Only when every pair is alike
-    (all allocations in one class) is one spare vector allocated and paired,
-    up to PLACEMENT_MAX_EXTRA; spares not chosen are freed.  Results never
-    depend on placement.  Returns ({name: tensor}, info) with the timing of
-    the allocation-order assignment ("default_ms") next to the chosen one."""
+    the remaining roles (5 launches each, scratch contents).  When the pair
+    times show two clusters (a >= 4 % gap), the fastest pair is cross-class
+    and is taken.  Otherwise every allocation so far is in one class: a spacer
+    block (2 GB, doubling each round, at most a quarter of free HBM in all) is
+    allocated to move past the current physical run, then one spare vector,
+    timed against the others — up to PLACEMENT_MAX_EXTRA spares.  Spacers and
+    unchosen spares are released to the driver at the end.  Results never
+    depend on placement.  Returns ({name: tensor}, info) with the time of the
+    allocation-order assignment ("default_ms") next to the chosen one."""
     import itertools
     import os
     f32 = dict(dtype=torch.float32, device=device)
@@ -151,7 +163,7 @@ def placed_vectors(n, device, names, method, max_extra=None):
     if max_extra is None:
         max_extra = int(os.environ.get("BDL_PLACEMENT_MAX_EXTRA", str(PLACEMENT_MAX_EXTRA)))
     free, _ = torch.cuda.mem_get_info(device)
-    max_extra = max(0, min(max_extra, int(0.25 * free // (n * 4))))
+    budget = int(0.25 * free)  # spacers + spares
     runs = build_runs([0], [n], [L.ATTR_PRIOR], n).to(device)
     it, im = names.index("theta"), names.index("mom")
     others = [i for i in range(len(names)) if i not in (it, im)]
@@ -164,28 +176,32 @@ def placed_vectors(n, device, names, method, max_extra=None):
             roles[names[i]] = vecs[j]
         return roles
 
-    times = {}
+    def timed(a, b):
+        return _time_launch(_placement_launcher(method, assign(a, b), n, device, runs), device)
+
     default = (it, im)
-    times[default] = _time_launch(_placement_launcher(method, assign(*default), n, device, runs),
-                                  device)
-    extra = 0
+    times = {default: timed(*default)}
+    spacers, skip, used, extra = [], PLACEMENT_SKIP0, 0, 0
     while True:
         for a, b in itertools.combinations(range(len(vecs)), 2):
             if (a, b) not in times and (b, a) not in times:
-                times[(a, b)] = _time_launch(
-                    _placement_launcher(method, assign(a, b), n, device, runs), device)
-        best = min(times, key=times.get)
-        if times[best] <= PLACEMENT_FAST * max(times.values()) or extra >= max_extra:
+                times[(a, b)] = timed(a, b)
+        if _two_classes(times.values()) or extra >= max_extra or used + skip + 4 * n > budget:
             break
-        vecs.append(torch.zeros(n, **f32))  # all alike so far: one more allocation
+        spacers.append(torch.empty(skip // 4, **f32))  # move past the current physical run
+        used += skip + 4 * n
+        skip *= 2
+        vecs.append(torch.zeros(n, **f32))
         extra += 1
+    best = min(times, key=times.get)
     chosen = assign(*best)
     out = {nm: chosen[nm] for nm in names}
-    keep = {id(t) for t in out.values()}
-    spare = [t for t in vecs if id(t) not in keep]
-    del vecs, chosen, spare  # unchosen spares return to torch's cache
+    del vecs, chosen, spacers
+    if extra:
+        torch.cuda.empty_cache()  # spacers and unchosen spares back to the driver
     return out, {"default_ms": round(times[default], 4), "chosen_ms": round(times[best], 4),
-                 "pairs_timed": len(times), "spares": extra, "method": method,
+                 "two_classes": _two_classes(times.values()), "pairs_timed": len(times),
+                 "spares": extra, "method": method,
                  "pairs_ms": sorted(round(t, 4) for t in times.values())}
 
 

@@ -17,6 +17,6 @@ run() {  # name seconds cmd...
 STEPS=${STEPS:-smoke,tests,bench}
 rc_all=0
 if [[ $STEPS == *smoke* ]]; then run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || rc_all=1; fi
-if [[ $STEPS == *tests* ]]; then run pytest_gpu 1200 python -m pytest tests -m gpu -q -rfE ${PYTEST_ARGS:-} || rc_all=1; fi
-if [[ $STEPS == *bench* ]]; then run bench 900 python bench.py ${BENCH_ARGS:-} || rc_all=1; fi
+if [[ $STEPS == *tests* ]]; then run pytest_gpu 1000 python -u -m pytest tests -m gpu -v -rfE --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} || rc_all=1; fi
+if [[ $STEPS == *bench* ]]; then run bench 400 python bench.py ${BENCH_ARGS:-} || rc_all=1; fi
 exit $rc_all
