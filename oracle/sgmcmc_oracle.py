@@ -227,12 +227,14 @@ def _cat(ts):
     return torch.cat([t.reshape(-1) for t in ts]).numpy().copy()
 
 
-def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
+def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn,
+             record_steps=True):
     """Run the reference Runner loop for cfg['method'] on prescribed grads/noise.
 
     grad_fn(t) -> flat np.float32 gradient of step t; noise_fn(t) -> flat
     np.float32 standard-normal draws of step t (named_parameters order).
-    Returns a dict shaped like the golden fixtures.
+    Returns a dict shaped like the golden fixtures.  record_steps=False keeps
+    only the final theta / momentum (config-size runs: 44.5 M parameters).
     """
     method = cfg["method"]
     hp = {k: str(v) for k, v in cfg["hparams"].items()}
@@ -291,15 +293,18 @@ def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
                 lrs = [lr, lr * (lr_head0 / lr0)]
                 rec["lrs"].append([float(x) for x in lrs])
                 rec["should_sample"].append(bool(ss) if method == "csghmc" else False)
-                rec["theta"].append(_cat(params))
+                if record_steps:
+                    rec["theta"].append(_cat(params))
                 g, eps = grads_now(step), noise_now(step)
                 if method == "csghmc":
-                    rec["mom"].append(_cat(moms))
+                    if record_steps:
+                        rec["mom"].append(_cat(moms))
                     moms = csghmc_update(params, g, moms, names, readout, lrs, prior_sig, alpha, N,
                                          nd, ss, eps)
                 elif adam:  # adam_csghmc.py:312-322: Model, clip, SGD(momentum 0)
-                    rec["mom"].append(_cat(moms))
-                    adam_rec()
+                    if record_steps:
+                        rec["mom"].append(_cat(moms))
+                        adam_rec()
                     at += 1
                     newg, moms, am, av = adam_sghmc_model(
                         params, params0, g, moms, am, av, names, readout, lrs, prior_sig, bias,
@@ -309,8 +314,9 @@ def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
                     sgd_step(params, newg, [None] * len(params),
                              [lrs[1] if h else lrs[0] for h in is_head], 0.0)
                 else:
-                    rec["mom"].append(_cat([torch.zeros_like(p) if bb is None else bb
-                                            for p, bb in zip(params, bufs)]))
+                    if record_steps:
+                        rec["mom"].append(_cat([torch.zeros_like(p) if bb is None else bb
+                                                for p, bb in zip(params, bufs)]))
                     newg = sgld_model(params, params0, g, names, readout, lrs, prior_sig, bias, N,
                                       nd, eps)
                     if cfg.get("clip_grad") is not None:  # csgld.py:250-251
@@ -393,24 +399,28 @@ def simulate(cfg, segments, readout, theta_init, prior_mean, grad_fn, noise_fn):
         for b in range(bpe):
             rec["lrs"].append([float(x) for x in lrs])
             rec["should_sample"].append(False)
-            rec["theta"].append(_cat(params))
+            if record_steps:
+                rec["theta"].append(_cat(params))
             g, eps = grads_now(step), noise_now(step)
             if method == "sghmc":
-                rec["mom"].append(_cat(moms))
+                if record_steps:
+                    rec["mom"].append(_cat(moms))
                 newg, moms = sghmc_model(params, params0, g, moms, names, readout, lrs, prior_sig,
                                          bias, alpha, N, nd, eps)
             elif adam:  # adam_sghmc.py:458-553, then SGD(args.momentum) (:60, :229)
-                rec["mom"].append(_cat(moms))
-                adam_rec()
-                rec.setdefault("sgd_buf", []).append(_cat([torch.zeros_like(p) if bb is None
-                                                           else bb for p, bb in zip(params, bufs)]))
+                if record_steps:
+                    rec["mom"].append(_cat(moms))
+                    adam_rec()
+                    rec.setdefault("sgd_buf", []).append(_cat([torch.zeros_like(p) if bb is None
+                                                               else bb for p, bb in zip(params, bufs)]))
                 at += 1
                 newg, moms, am, av = adam_sghmc_model(
                     params, params0, g, moms, am, av, names, readout, lrs, prior_sig, bias, alpha,
                     b1, b2, aeps, at, N, nd, eps)
             else:
-                rec["mom"].append(_cat([torch.zeros_like(p) if bb is None else bb
-                                        for p, bb in zip(params, bufs)]))
+                if record_steps:
+                    rec["mom"].append(_cat([torch.zeros_like(p) if bb is None else bb
+                                            for p, bb in zip(params, bufs)]))
                 newg = sgld_model(params, params0, g, names, readout, lrs, prior_sig, bias, N, nd,
                                   eps)
             bufs = sgd_step(params, newg, bufs, lr_per_param, momentum)

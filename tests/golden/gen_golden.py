@@ -524,6 +524,122 @@ def run_ckpt_interop(methods, method, cfg):
                 eval_draws=np.int64(draws))
 
 
+# --------------------------------------------------------------------------
+# Config-size pins: the reference Runners' own step
+# loop on a FakeNet with the REAL parameter shapes of the config's backbone
+# (mlp_mnist: 8 tensors, 2,797,010; ResNet-101 C=1000: 314 tensors,
+# 44,549,160 — bayesdll_amd/shapes.py), prescribed gradients
+# (fakenet.grads_for_step) and the deterministic det_normal stream in place
+# of torch.randn_like (one draw per tensor per step, counter k).  The vectors
+# are too large to store: the fixture keeps a 4096-element index subsample,
+# float64 norms and a SHA-256 of the exact fp32 bytes of every final vector.
+# --------------------------------------------------------------------------
+FULLSIZE_CONFIGS = {
+    # config 2: mlp_mnist cSGHMC (pretrain_resnet101.py:127 hparams; ND = MNIST 60k x 0.5)
+    "fullsize_c2_csghmc": ("csghmc", "mlp_mnist", 10, dict(
+        epochs=4, bpe=5, num_cycles=2, beta=0.5, lr=1e-2, lr_head=1e-2, ND=30000, init_seed=41,
+        init_scale=0.03, grad_seed=42, grad_scale=1e-2, noise_seed=43,
+        hparams=dict(prior_sig=1.0, bias="informative", momentum_decay=0.18, Ninflate=1.0,
+                     nd=0.01, burnin=0, thin=2, nst=5))),
+    # config 3: ResNet-101 (C=1000) SGLD + SGD(momentum 0.5), informative prior
+    # theta0 ~ N(0, 0.02^2) (the IMAGENET1K_V1 stand-in), theta = theta0 +
+    # N(0, 1e-3^2), g ~ N(0, 1e-3^2), ND = Pets trainval x 0.5 (README.md:111)
+    "fullsize_c3_sgld": ("sgld", "resnet101", 1000, dict(
+        epochs=3, bpe=4, lr=1e-4, lr_head=1e-2, momentum=0.5, ND=1840, init_seed=44,
+        init_scale=1e-3, prior_seed=45, prior_scale=0.02, grad_seed=46, grad_scale=1e-3,
+        noise_seed=47,
+        hparams=dict(prior_sig=1.0, bias="informative", Ninflate=1e3, nd=0.01, burnin=1,
+                     thin=2, nst=2))),
+}
+
+
+def vec_digest(v):
+    import hashlib
+    v = np.ascontiguousarray(np.asarray(v, np.float32))
+    return dict(sha=hashlib.sha256(v.tobytes()).hexdigest(),
+                norm=np.float64(np.linalg.norm(v.astype(np.float64))))
+
+
+def run_fullsize(methods, method, backbone, num_classes, cfg):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from bayesdll_amd.shapes import segments
+    segs, readout = segments(backbone, num_classes)
+    n = numel_of(segs)
+    theta_init = init_vector(cfg["init_seed"], n, cfg["init_scale"])
+    net0, prior = None, None
+    if cfg.get("prior_seed") is not None:
+        prior = init_vector(cfg["prior_seed"], n, cfg["prior_scale"])
+        theta_init = (prior + theta_init).astype(np.float32)  # theta = theta0 + N(0, s^2)
+        net0 = FakeNet(segs, readout, init=prior)
+    net = FakeNet(segs, readout, grad_seed=cfg["grad_seed"], grad_scale=cfg["grad_scale"],
+                  init=theta_init)
+    tmp = tempfile.mkdtemp(prefix="bdl_golden_full_")
+    args = make_args(tmp, pretrained=("fake" if net0 is not None else None), epochs=cfg["epochs"],
+                     num_cycles=cfg.get("num_cycles", 2), lr=cfg["lr"], lr_head=cfg["lr_head"],
+                     momentum=cfg.get("momentum", 0.0), ND=cfg["ND"],
+                     proportion_exploration=cfg.get("beta", 0.5), num_classes=num_classes,
+                     hparams={k: str(v) for k, v in cfg["hparams"].items()})
+    mod = getattr(methods, method)
+    runner = mod.Runner(net, net0, args, logging.getLogger("golden"))
+    counter = [0]
+    orig = torch.randn_like
+
+    def det_randn_like(t, *a, **k):
+        out = torch.from_numpy(det_normal(cfg["noise_seed"], counter[0], t.numel())).reshape(t.shape)
+        counter[0] += 1
+        return out.to(t.dtype)
+
+    torch.randn_like = det_randn_like
+    try:
+        loader = fake_loader(cfg["bpe"])
+        if method == "csghmc":
+            for ep in range(cfg["epochs"]):
+                runner.cyclical_scheduler.current_epoch = ep
+                runner.train_one_epoch(loader)
+        else:  # sgld: Runner.train's epoch loop minus evaluation (methods/sgld.py:193-250)
+            bi = 0
+            for ep in range(cfg["epochs"]):
+                if ep == runner.burnin:
+                    with torch.no_grad():
+                        tv = torch.nn.utils.parameters_to_vector(runner.net.parameters())
+                        runner.post_theta_mom1 = tv * 1.0
+                        if runner.nst > 0:
+                            runner.post_theta_mom2 = tv ** 2
+                    runner.post_theta_cnt = 1
+                _, _, bi = runner.train_one_epoch(loader, collect=(ep >= runner.burnin), bi=bi)
+    finally:
+        torch.randn_like = orig
+    idx = subset_idx(n)
+    names = [nm for nm, _ in runner.net.named_parameters()]
+    vecs = {"theta": flat(runner.net.parameters())}
+    if method == "csghmc":
+        vecs["mom"] = torch.cat([runner.model.momentum_buffer[nm].reshape(-1)
+                                 for nm in names]).numpy()
+        cyc = sorted(runner.cycle_theta_mom1.keys())
+        for c in cyc:
+            vecs[f"cycle{c}_mom1"] = runner.cycle_theta_mom1[c].numpy()
+            vecs[f"cycle{c}_mom2"] = runner.cycle_theta_mom2[c].numpy()
+        extra = dict(cycles=np.array(cyc, np.int64),
+                     samples_per_cycle=np.array([runner.samples_per_cycle[c] for c in cyc]),
+                     samples_collected=np.int64(runner.samples_collected),
+                     current_cycle=np.int64(runner.current_cycle))
+    else:
+        vecs["mom"] = np.concatenate([runner.optimizer.state[p]["momentum_buffer"].reshape(-1).numpy()
+                                      for p in runner.net.parameters()])
+        vecs["post_mom1"] = runner.post_theta_mom1.numpy()
+        vecs["post_mom2"] = runner.post_theta_mom2.numpy()
+        extra = dict(post_cnt=np.int64(runner.post_theta_cnt))
+    out = dict(config=json.dumps(dict(cfg, method=method, backbone=backbone,
+                                      num_classes=num_classes)),
+               n=np.int64(n), idx=idx, draws=np.int64(counter[0]), **extra)
+    for key, v in vecs.items():
+        d = vec_digest(v)
+        out[f"{key}_sub"] = np.asarray(v, np.float32)[idx]
+        out[f"{key}_sha"] = d["sha"]
+        out[f"{key}_norm"] = d["norm"]
+    return out
+
+
 def calibration_fixture():
     """Reference calibration.analyze / find_optimal_temperature on seeded
     logits (the metrics the Runners log after a new best evaluation)."""
@@ -572,6 +688,14 @@ def main():
             print(f"wrote ckpt_ref_{method}.pt epoch={int(rec['epoch'])} "
                   f"eval_draws={int(rec['eval_draws'])} loss={float(rec['eval_loss']):.6f}")
         np.savez_compressed(os.path.join(HERE, "ckpt_ref.npz"), **recs)
+        return
+    if only == "fullsize":
+        torch.set_num_threads(8)
+        for name, (method, backbone, classes, cfg) in FULLSIZE_CONFIGS.items():
+            rec = run_fullsize(methods, method, backbone, classes, copy.deepcopy(cfg))
+            np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **rec)
+            print(f"wrote {name}.npz n={int(rec['n'])} draws={int(rec['draws'])} "
+                  f"theta_norm={float(rec['theta_norm']):.6f}")
         return
     if only == "mlp":
         torch.set_num_threads(8)

@@ -58,3 +58,67 @@ def test_schedule_tables_match_reference():
         np.testing.assert_array_equal(np.array(ss), d[key + "_sample"])
         np.testing.assert_array_equal(np.array(last), d[key + "_last"])
         np.testing.assert_array_equal(np.array(cyc), d[key + "_cycle"])
+
+
+def _fullsize_noise_fn(fx, segments):
+    """Draw indices of the generator's det_normal stream: one per tensor per
+    step, plus — for csghmc — the nst posterior draws per tensor that
+    Runner.full_batch_likelihoods takes at every cycle end
+    (methods/csghmc.py:358-372, :568-638), which the oracle's step loop skips."""
+    from fakenet import det_normal
+    cfg = fx["config"]
+    hp = cfg["hparams"]
+    numels = [int(np.prod(s)) for _, s in segments]
+    T = len(numels)
+    bases, k = [], 0
+    if cfg["method"] == "csghmc":
+        sched = O.CyclicalSchedule(cfg["lr"], cfg["num_cycles"], cfg["epochs"], cfg["beta"])
+        for ep in range(cfg["epochs"]):
+            for b in range(cfg["bpe"]):
+                bases.append(k)
+                k += T
+                if sched.last_in_cycle(ep, b, cfg["bpe"]):
+                    k += int(hp["nst"]) * T
+    else:
+        bases = [T * t for t in range(cfg["epochs"] * cfg["bpe"])]
+    return lambda t: np.concatenate([det_normal(cfg["noise_seed"], bases[t] + i, n)
+                                     for i, n in enumerate(numels)])
+
+
+@pytest.mark.parametrize("name", ["fullsize_c2_csghmc", "fullsize_c3_sgld"])
+def test_oracle_matches_reference_at_config_size(name):
+    """SURVEY §8(d) C2 (mlp_mnist, 2,797,010 params, cSGHMC) and C3 (ResNet-101
+    C=1000, 44,549,160 params, SGLD + SGD momentum): the oracle run on the
+    real shapes lands on the reference's exact final bytes (SHA-256 of every
+    final vector, tests/golden/gen_golden.py FULLSIZE_CONFIGS)."""
+    import hashlib
+    from bayesdll_amd.shapes import segments
+    from fakenet import grads_for_step, init_vector
+    fx = load(name)
+    cfg = fx["config"]
+    segs, readout = segments(cfg["backbone"], cfg["num_classes"])
+    n = int(fx["n"])
+    theta_init = init_vector(cfg["init_seed"], n, cfg["init_scale"])
+    prior = np.zeros(n, np.float32)
+    if cfg.get("prior_seed") is not None:
+        prior = init_vector(cfg["prior_seed"], n, cfg["prior_scale"])
+        theta_init = (prior + theta_init).astype(np.float32)
+    out = O.simulate(cfg, segs, readout, theta_init, prior,
+                     lambda t: grads_for_step(cfg["grad_seed"], t, n, cfg["grad_scale"]),
+                     _fullsize_noise_fn(fx, segs), record_steps=False)
+    vecs = {"theta": out["theta"][-1], "mom": out["mom"][-1]}
+    if cfg["method"] == "csghmc":
+        for i, c in enumerate(out["cycles"]):
+            vecs[f"cycle{c}_mom1"] = out["cycle_mom1"][i]
+            vecs[f"cycle{c}_mom2"] = out["cycle_mom2"][i]
+        np.testing.assert_array_equal(out["samples_per_cycle"], fx["samples_per_cycle"])
+    else:
+        vecs["post_mom1"], vecs["post_mom2"] = out["post_mom1"], out["post_mom2"]
+        assert out["post_cnt"] == int(fx["post_cnt"])
+    keys = sorted(k[:-4] for k in fx if k.endswith("_sha"))
+    assert sorted(vecs) == keys
+    for key in keys:
+        v = np.ascontiguousarray(vecs[key], np.float32)
+        assert v.size == n
+        np.testing.assert_array_equal(v[fx["idx"]], fx[f"{key}_sub"], err_msg=key)
+        assert hashlib.sha256(v.tobytes()).hexdigest() == str(fx[f"{key}_sha"]), key
