@@ -33,6 +33,7 @@
 // method, compiled in parallel), this file (host entry points of the C-ABI,
 // validation, launch geometry, the clip-norm / moments / sample kernels).
 #include "bdl_kernels.hpp"
+#include "bdl_placement.h"
 
 namespace bdl {
 namespace {
@@ -880,6 +881,102 @@ int bdl_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t chain, uint
     g_last_error = std::string("bdl_philox_normal: launch failed: ") + hipGetErrorString(err);
     return BDL_ERR_LAUNCH;
   }
+  return BDL_OK;
+}
+
+
+// ---------------------------------------------------------------------------
+// Physical-chunk placement (include/bdl_placement.h).  Host-only: hipMemCreate
+// physical chunks, mapped into contiguous virtual ranges with hipMemMap.  The
+// Python side (flat.placed_vectors) times chunk pairs with the production
+// kernel and maps theta / momentum from chunks that pair fast.
+static hipMemAllocationProp chunk_prop(int32_t device) {
+  hipMemAllocationProp prop;
+  memset(&prop, 0, sizeof prop);
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = device;
+  return prop;
+}
+
+static int hip_fail(const char* what, hipError_t e) {
+  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  return BDL_ERR_LAUNCH;
+}
+
+int bdl_chunk_granularity(int32_t device, uint64_t* bytes) {
+  if (!bytes) return fail(BDL_ERR_NULL, "bdl_chunk_granularity: null out");
+  hipMemAllocationProp prop = chunk_prop(device);
+  size_t g = 0;
+  const hipError_t e = hipMemGetAllocationGranularity(&g, &prop,
+                                                      hipMemAllocationGranularityRecommended);
+  if (e != hipSuccess) return hip_fail("bdl_chunk_granularity", e);
+  *bytes = g;
+  return BDL_OK;
+}
+
+int bdl_chunk_create(int32_t device, uint64_t bytes, uint64_t* handle) {
+  if (!handle) return fail(BDL_ERR_NULL, "bdl_chunk_create: null out");
+  if (bytes == 0) return fail(BDL_ERR_ARG, "bdl_chunk_create: zero bytes");
+  hipMemAllocationProp prop = chunk_prop(device);
+  hipMemGenericAllocationHandle_t h;
+  const hipError_t e = hipMemCreate(&h, bytes, &prop, 0);
+  if (e != hipSuccess) return hip_fail("bdl_chunk_create: hipMemCreate", e);
+  static_assert(sizeof(h) <= sizeof(uint64_t), "allocation handle wider than 64 bits");
+  uint64_t out = 0;
+  memcpy(&out, &h, sizeof h);
+  *handle = out;
+  return BDL_OK;
+}
+
+int bdl_chunk_release(uint64_t handle) {
+  hipMemGenericAllocationHandle_t h;
+  memcpy(&h, &handle, sizeof h);
+  const hipError_t e = hipMemRelease(h);
+  if (e != hipSuccess) return hip_fail("bdl_chunk_release: hipMemRelease", e);
+  return BDL_OK;
+}
+
+int bdl_vmm_map(int32_t device, const uint64_t* handles, int32_t nchunks, uint64_t chunk_bytes,
+                void** va) {
+  if (!handles || !va) return fail(BDL_ERR_NULL, "bdl_vmm_map: null argument");
+  if (nchunks <= 0 || chunk_bytes == 0) return fail(BDL_ERR_ARG, "bdl_vmm_map: empty range");
+  const size_t total = (size_t)nchunks * (size_t)chunk_bytes;
+  void* base = nullptr;
+  hipError_t e = hipMemAddressReserve(&base, total, (size_t)2 << 20, nullptr, 0);
+  if (e != hipSuccess) return hip_fail("bdl_vmm_map: hipMemAddressReserve", e);
+  int32_t mapped = 0;
+  for (; mapped < nchunks; ++mapped) {
+    hipMemGenericAllocationHandle_t h;
+    memcpy(&h, &handles[mapped], sizeof h);
+    e = hipMemMap((char*)base + (size_t)mapped * chunk_bytes, chunk_bytes, 0, h, 0);
+    if (e != hipSuccess) break;
+  }
+  if (e == hipSuccess) {
+    hipMemAccessDesc acc;
+    memset(&acc, 0, sizeof acc);
+    acc.location.type = hipMemLocationTypeDevice;
+    acc.location.id = device;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    e = hipMemSetAccess(base, total, &acc, 1);
+    if (e == hipSuccess) {
+      *va = base;
+      return BDL_OK;
+    }
+  }
+  const int rc = hip_fail("bdl_vmm_map: hipMemMap/hipMemSetAccess", e);
+  for (int32_t i = 0; i < mapped; ++i)
+    (void)hipMemUnmap((char*)base + (size_t)i * chunk_bytes, chunk_bytes);
+  (void)hipMemAddressFree(base, total);
+  return rc;
+}
+
+int bdl_vmm_unmap(void* va, uint64_t total_bytes) {
+  if (!va) return fail(BDL_ERR_NULL, "bdl_vmm_unmap: null va");
+  hipError_t e = hipMemUnmap(va, total_bytes);
+  if (e != hipSuccess) return hip_fail("bdl_vmm_unmap: hipMemUnmap", e);
+  e = hipMemAddressFree(va, total_bytes);
+  if (e != hipSuccess) return hip_fail("bdl_vmm_unmap: hipMemAddressFree", e);
   return BDL_OK;
 }
 

@@ -73,11 +73,6 @@ def build_runs(offsets, numels, attrs, n):
 PLACEMENT_MIN_ELEMS = 1 << 24  # below ~64 MB per vector placement effects are noise
 
 
-PLACEMENT_GAP = 1.04      # two placement classes seen: a gap of >= 4 % in the sorted pair times
-PLACEMENT_MAX_EXTRA = 4   # at most this many spare vectors are allocated while pairing
-PLACEMENT_SKIP0 = 2 << 30  # first spacer allocated ahead of a spare (doubles each round)
-
-
 def _placement_launcher(method, vs, n, device, runs):
     """The sampler's production kernel on scratch vectors `vs` (role -> tensor)."""
     from types import SimpleNamespace
@@ -114,95 +109,43 @@ def _time_launch(launch, device, reps=5):
     return float(np.median([a.elapsed_time(b) for a, b in ev]))
 
 
-def _two_classes(times):
-    """Do the timed (theta, mom) pairings fall into a fast and a slow cluster?
-    (The clusters are 6-10 % apart; pairs inside one class spread by <= 3 %.)"""
-    t = sorted(times)
-    return any(b > PLACEMENT_GAP * a for a, b in zip(t, t[1:]))
-
-
-def placed_vectors(n, device, names, method, max_extra=None):
+def placed_vectors(n, device, names, method):
     """Allocate the chain's swept fp32 vectors (`names` among theta, grad, mom,
-    prior, extra state) and choose WHICH allocation plays which role so that
-    the two vectors the step rewrites in place — theta and mom — sit in
-    different physical placement classes.
-
-    What was measured (profiles/round2/placement/, tools/placement_probe2.cpp,
-    the production explore kernel on ViT-L/32-sized vectors): the sweep is
-    bimodal, 0.955-0.97 ms or 1.04-1.10 ms, and which one is decided by ONE
-    thing — whether theta and mom (the two read-modify-write streams) are in
-    the same placement class.  Every ordered (theta, grad, mom) triple of 9
-    allocations (role_mix/): fast iff class(theta) != class(mom); the
-    read-only gradient's class never matters.  The class is a property of the
-    physical memory an allocation lands on, invisible from user space: moving
-    mom by 256 B ... 1 GB inside its allocation never changes it
-    (mom_offset_*), physically contiguous allocations and VMM-mapped 1 GB
-    chunks are as bimodal as hipMalloc (VMM 2 MB chunks land in between: a mix
-    of classes along the vector; allocators/), and the classes come
-    in runs of several GB in allocation order (class_map/) — which is why
-    consecutive allocations so often pair badly.
-
-    So the choice is a role assignment, not a lottery over fresh sets: the
-    vectors are allocated once; for every unordered pair of allocations the
-    method's kernel is timed with that pair as (theta, mom) and the others in
-    the remaining roles (5 launches each, scratch contents).  When the pair
-    times show two clusters (a >= 4 % gap), the fastest pair is cross-class
-    and is taken.  Otherwise every allocation so far is in one class: a spacer
-    block (2 GB, doubling each round, at most a quarter of free HBM in all) is
-    allocated to move past the current physical run, then one spare vector,
-    timed against the others — up to PLACEMENT_MAX_EXTRA spares.  Spacers and
-    unchosen spares are released to the driver at the end.  Results never
-    depend on placement.  Returns ({name: tensor}, info) with the time of the
-    allocation-order assignment ("default_ms") next to the chosen one."""
-    import itertools
+    prior, extra state), zeroed.  With `method` (the sampler's kernel family)
+    and vectors of >= PLACEMENT_MIN_ELEMS, they are built from physical chunks
+    with theta and mom paired fast (bayesdll_amd.placement; DESIGN.md §4
+    "Placement"); otherwise, or when the driver refuses chunk mappings, from
+    torch's allocator.  BDL_PLACEMENT: "search" (default), "order" (chunks in
+    allocation order, no pair timing), "0" (torch's allocator).
+    Returns ({name: tensor}, info or None)."""
     import os
     f32 = dict(dtype=torch.float32, device=device)
-    vecs = [torch.zeros(n, **f32) for _ in names]
-    if method is None or n < PLACEMENT_MIN_ELEMS or "mom" not in names or "theta" not in names:
-        return dict(zip(names, vecs)), None
-    if max_extra is None:
-        max_extra = int(os.environ.get("BDL_PLACEMENT_MAX_EXTRA", str(PLACEMENT_MAX_EXTRA)))
+    mode = os.environ.get("BDL_PLACEMENT", "search")
+    if mode not in ("search", "order", "0"):
+        raise ValueError(f"BDL_PLACEMENT must be search, order or 0, got {mode!r}")
+    if method is None or n < PLACEMENT_MIN_ELEMS or "mom" not in names or "theta" not in names \
+            or mode == "0":
+        return {nm: torch.zeros(n, **f32) for nm in names}, None
+    from . import placement as P
     free, _ = torch.cuda.mem_get_info(device)
-    budget = int(0.25 * free)  # spacers + spares
-    runs = build_runs([0], [n], [L.ATTR_PRIOR], n).to(device)
-    it, im = names.index("theta"), names.index("mom")
-    others = [i for i in range(len(names)) if i not in (it, im)]
+    runs_by_n = {}
 
-    def assign(a, b):
-        """theta = vecs[a], mom = vecs[b], the other roles in allocation order."""
-        rest = [j for j in range(len(vecs)) if j not in (a, b)]
-        roles = {"theta": vecs[a], "mom": vecs[b]}
-        for i, j in zip(others, rest):
-            roles[names[i]] = vecs[j]
-        return roles
+    def launcher(roles, m):
+        if m not in runs_by_n:
+            runs_by_n[m] = build_runs([0], [m], [L.ATTR_PRIOR], m).to(device)
+        return _placement_launcher(method, roles, m, device, runs_by_n[m])
 
-    def timed(a, b):
-        return _time_launch(_placement_launcher(method, assign(a, b), n, device, runs), device)
-
-    default = (it, im)
-    times = {default: timed(*default)}
-    spacers, skip, used, extra = [], PLACEMENT_SKIP0, 0, 0
-    while True:
-        for a, b in itertools.combinations(range(len(vecs)), 2):
-            if (a, b) not in times and (b, a) not in times:
-                times[(a, b)] = timed(a, b)
-        if _two_classes(times.values()) or extra >= max_extra or used + skip + 4 * n > budget:
-            break
-        spacers.append(torch.empty(skip // 4, **f32))  # move past the current physical run
-        used += skip + 4 * n
-        skip *= 2
-        vecs.append(torch.zeros(n, **f32))
-        extra += 1
-    best = min(times, key=times.get)
-    chosen = assign(*best)
-    out = {nm: chosen[nm] for nm in names}
-    del vecs, chosen, spacers
-    if extra:
-        torch.cuda.empty_cache()  # spacers and unchosen spares back to the driver
-    return out, {"default_ms": round(times[default], 4), "chosen_ms": round(times[best], 4),
-                 "two_classes": _two_classes(times.values()), "pairs_timed": len(times),
-                 "spares": extra, "method": method,
-                 "pairs_ms": sorted(round(t, 4) for t in times.values())}
+    try:
+        vecs, info = P.place(n, device, names, launcher, lambda f: _time_launch(f, device, 3),
+                             budget_bytes=int(0.25 * free), search=mode == "search")
+    except RuntimeError as e:  # chunk mappings unavailable: plain allocations
+        import warnings
+        warnings.warn(f"bayesdll_amd: physical-chunk placement unavailable ({e}); "
+                      "using torch's allocator")
+        return {nm: torch.zeros(n, **f32) for nm in names}, {"allocator": "torch",
+                                                             "error": str(e)[:200]}
+    info["method"] = method
+    return vecs, info
 
 
 GRAD_MODES = ("tensor", "flat")

@@ -1,0 +1,52 @@
+/* bdl_placement.h — physical-chunk placement of the chain's swept vectors.
+ *
+ * Not part of the reference's interface: the reference keeps every vector in
+ * torch's caching allocator (methods/csghmc.py:727-730 momentum_buffer,
+ * methods/sgld.py:98 parameters_to_vector).  On MI355X the fused step's HBM
+ * rate depends on which PHYSICAL memory the two vectors it rewrites in place
+ * (theta and the momentum / SGD buffer) land on: the same sweep runs ~0.95 ms
+ * or ~1.05 ms for ViT-L/32 depending on the pair of physical regions
+ * (profiles/round2/placement/, DESIGN.md §4 "Placement").  These entry points
+ * let the host allocate physical chunks (hipMemCreate), time pairs of them,
+ * and map the chosen chunks into one contiguous virtual range per vector
+ * (hipMemAddressReserve + hipMemMap), so the pairing is chosen chunk by chunk
+ * instead of drawn by the allocator.
+ *
+ * Ownership: a chunk handle is released with bdl_chunk_release once it is
+ * mapped where it is needed (the physical memory lives until its last mapping
+ * is unmapped); a mapping is removed with bdl_vmm_unmap after all work that
+ * reads it has completed (the caller synchronises).  Errors: negative
+ * bdl_status (bdl_sgmcmc.h) and bdl_last_error(). */
+#ifndef BDL_PLACEMENT_H
+#define BDL_PLACEMENT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Allocation granularity (bytes) of physical chunks on `device`; chunk sizes
+ * passed below must be multiples of it. */
+int bdl_chunk_granularity(int32_t device, uint64_t* bytes);
+
+/* Create one physical chunk of `bytes` on `device` (not yet mapped). */
+int bdl_chunk_create(int32_t device, uint64_t bytes, uint64_t* handle);
+
+/* Drop the caller's reference to a chunk (freed when no mapping remains). */
+int bdl_chunk_release(uint64_t handle);
+
+/* Reserve nchunks * chunk_bytes of virtual address space (2 MiB aligned), map
+ * handles[i] at offset i * chunk_bytes, grant `device` read/write; *va
+ * receives the base.  A chunk may be mapped at several places. */
+int bdl_vmm_map(int32_t device, const uint64_t* handles, int32_t nchunks, uint64_t chunk_bytes,
+                void** va);
+
+/* Unmap and free a range returned by bdl_vmm_map (total = nchunks * chunk_bytes). */
+int bdl_vmm_unmap(void* va, uint64_t total_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BDL_PLACEMENT_H */

@@ -11,15 +11,19 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "bdl_sgmcmc.h")
+HEADERS = [HEADER, os.path.join(ROOT, "include", "bdl_placement.h")]
 
 
-def declared_functions():
-    txt = open(HEADER).read()
+def declared_functions(headers=HEADERS):
+    txt = "".join(open(h).read() for h in headers)
     return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(bdl_\w+)\(", txt, re.M)))
 
 
 def test_header_declares_expected_api():
-    assert declared_functions() == sorted([
+    assert declared_functions([HEADERS[1]]) == sorted([
+        "bdl_chunk_granularity", "bdl_chunk_create", "bdl_chunk_release", "bdl_vmm_map",
+        "bdl_vmm_unmap"])
+    assert declared_functions([HEADER]) == sorted([
         "bdl_version", "bdl_last_error", "bdl_build_runs", "bdl_sgmcmc_step",
         "bdl_moments_update", "bdl_posterior_sample", "bdl_philox_normal",
         "bdl_set_launch_config", "bdl_clip_workspace_bytes", "bdl_sgld_step_clipped", "bdl_adam_step"])

@@ -580,11 +580,13 @@ def test_full_size_vit_sghmc_matches_torch():
 
 
 def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
-    """flat.placed_vectors: every (theta, mom) pairing of the allocations is
-    timed and the fastest kept; the update itself never depends on where the
-    vectors live."""
+    """flat.placed_vectors (bayesdll_amd.placement): the vectors are built from
+    physical chunks mapped into one range each, every (theta, mom) chunk
+    pairing is timed, the faster of the chosen / allocation-order assignment
+    is kept, and the update itself never depends on where the vectors live."""
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
+    from bayesdll_amd import placement as P
     from bayesdll_amd.flat import FlatState, PLACEMENT_MIN_ELEMS
     segs = [("l0.weight", (PLACEMENT_MIN_ELEMS + 3,)), ("fc.weight", (1024,))]
     outs = []
@@ -594,12 +596,19 @@ def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
             assert st.placement_info is None
         else:
             info = st.placement_info
-            assert info["pairs_timed"] >= 3  # theta, grad, mom: three pairings at least
-            assert info["chosen_ms"] == min(info["pairs_ms"])
+            assert info["allocator"] == "vmm", info
+            per, cb = P.chunk_geometry(st.n)
+            assert info["chunks_per_vector"] == per == 1
+            assert info["chunks_allocated"] >= 3 * per + 2 * per
+            assert info["pairs_timed"] == info["chunks_allocated"] * (info["chunks_allocated"] - 1)
             assert info["chosen_ms"] <= info["default_ms"]
-            assert 0 <= info["spares"] <= 4
+            assert info["theta_chunks"] != info["mom_chunks"]
             ptrs = {st.theta.data_ptr(), st.grad.data_ptr(), st.mom.data_ptr()}
             assert len(ptrs) == 3
+            for v in (st.theta, st.grad, st.mom):
+                assert v.is_cuda and v.numel() == st.n
+                assert v.data_ptr() % (2 << 20) == 0
+                assert not v.any()  # zeroed
         g = torch.Generator(device=DEV).manual_seed(0)
         st.theta.normal_(0, 0.02, generator=g)
         st.grad.normal_(0, 1e-3, generator=g)
@@ -611,6 +620,53 @@ def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
         torch.cuda.synchronize()
         outs.append((st.theta.clone(), st.mom.clone()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_chunk_mapping_lifetime():
+    """A mapped range lives as long as any tensor viewing it (parameters are
+    views into theta) and is unmapped when the last one goes; the physical
+    chunk survives its handle's release while mapped; a range freed during a
+    graph capture is unmapped after it, not inside it."""
+    import ctypes as C
+    import gc
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import placement as P
+    lib = L.lib()
+    gran = C.c_uint64()
+    L.check(lib.bdl_chunk_granularity(0, C.byref(gran)), "granularity")
+    assert gran.value > 0 and (2 << 20) % gran.value == 0
+    cb = 4 << 20
+    hs = []
+    for _ in range(2):
+        h = C.c_uint64()
+        L.check(lib.bdl_chunk_create(0, cb, C.byref(h)), "create")
+        hs.append(h.value)
+    t = P.Mapping(0, hs, cb, 2 * cb // 4).tensor()
+    for h in hs:
+        L.check(lib.bdl_chunk_release(h), "release")  # mapped: stays alive
+    t.copy_(torch.arange(t.numel(), device=DEV, dtype=torch.float32))
+    view = t[cb // 4 - 2: cb // 4 + 2].view(2, 2)  # straddles the two chunks
+    del t
+    gc.collect()
+    assert view.flatten().tolist() == [cb // 4 - 2, cb // 4 - 1, cb // 4, cb // 4 + 1]
+    # a range dropped inside a capture is queued, then unmapped after it
+    h = C.c_uint64()
+    L.check(lib.bdl_chunk_create(0, cb, C.byref(h)), "create")
+    m = P.Mapping(0, [h.value], cb, cb // 4)
+    L.check(lib.bdl_chunk_release(h.value), "release")
+    x = m.tensor()
+    del m
+    y = torch.zeros(4, device=DEV)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        y.add_(1.0)
+        del x  # last reference: the unmap must be deferred
+        assert len(P._pending) == 1
+    graph.replay()
+    torch.cuda.synchronize()
+    P.release_pending()
+    assert not P._pending and y.tolist() == [1.0] * 4
+    del view
 
 
 def test_full_size_vit_csghmc_sample_and_welford_collect_bitexact():

@@ -5,6 +5,7 @@
 //   write1  : 1 write stream
 //   copy    : 1 read + 1 write
 //   r3w2    : 3 reads + 2 writes (the explore step's mix, trivial arithmetic)
+//   r2w1    : 2 reads + 1 write to a third vector (the posterior-sample mix)
 // each with temporal / non-temporal access and several grid sizes, grid-stride,
 // 256-thread blocks, `U` float4 per lane in flight.
 #include <hip/hip_runtime.h>
@@ -53,10 +54,8 @@ __global__ __launch_bounds__(256) void probe(const f4* __restrict__ a, const f4*
       const long i = base + u * 256 + threadIdx.x;
       if (i < n4) {
         if (MODE != 1) ra[u] = ld<NT>(a + i);
-        if (MODE >= 3) {
-          rb[u] = ld<NT>(b + i);
-          rc[u] = ld<NT>(c + i);
-        }
+        if (MODE >= 3) rb[u] = ld<NT>(b + i);
+        if (MODE == 3 || MODE == 4) rc[u] = ld<NT>(c + i);
       }
     }
 #pragma unroll
@@ -66,7 +65,8 @@ __global__ __launch_bounds__(256) void probe(const f4* __restrict__ a, const f4*
       if (MODE == 0) acc += ra[u];
       if (MODE == 1) st<NT>(x + i, f4{1.f, 2.f, 3.f, 4.f});
       if (MODE == 2) st<NT>(x + i, ra[u]);
-      if (MODE >= 3) {
+      if (MODE == 5) st<NT>(x + i, ra[u] + rb[u] * 0.5f);
+      if (MODE == 3 || MODE == 4) {
         const f4 v = rc[u] * 0.82f - (ra[u] + rb[u]) * 1e-4f;
         // MODE 3: results to two other buffers; MODE 4: in place (a, c), as the sampler
         st<NT>(MODE == 3 ? x + i : const_cast<f4*>(a) + i, ra[u] + v);
@@ -107,7 +107,7 @@ float run(int grid, const f4* a, const f4* b, const f4* c, f4* x, f4* y, long n4
 template <int MODE, bool NT, int U, bool XCD = false>
 void sweep(const char* name, int cus, const f4* a, const f4* b, const f4* c, f4* x, f4* y, long n4,
            float* sink) {
-  const double bytes_per_el = (MODE == 0 || MODE == 1) ? 4 : (MODE == 2 ? 8 : 20);
+  const double bytes_per_el = (MODE == 0 || MODE == 1) ? 4 : (MODE == 2 ? 8 : (MODE == 5 ? 12 : 20));
   const int bpcs[] = {1, 2, 3, 4};
   for (int bpc : bpcs) {
     const float ms = run<MODE, NT, U, XCD>(cus * bpc, a, b, c, x, y, n4, sink, 20);
@@ -143,6 +143,17 @@ int main() {
       sweep<4, true, 4, true>("r3w2_inplace", cus, a, b, c, x, y, n4, sink);
       sweep<4, true, 2, false>("r3w2_inplace", cus, a, b, c, x, y, n4, sink);
       sweep<4, true, 2, true>("r3w2_inplace", cus, a, b, c, x, y, n4, sink);
+    }
+    CHECK(hipDeviceSynchronize());
+    return 0;
+  }
+  if (!strcmp(which, "r2w1")) {  // the posterior-sample mix
+    for (int rep = 0; rep < 2; ++rep) {
+      sweep<5, true, 1>("r2w1", cus, a, b, c, x, y, n4, sink);
+      sweep<5, true, 2>("r2w1", cus, a, b, c, x, y, n4, sink);
+      sweep<5, true, 4>("r2w1", cus, a, b, c, x, y, n4, sink);
+      sweep<5, false, 2>("r2w1", cus, a, b, c, x, y, n4, sink);
+      sweep<5, false, 4>("r2w1", cus, a, b, c, x, y, n4, sink);
     }
     CHECK(hipDeviceSynchronize());
     return 0;
