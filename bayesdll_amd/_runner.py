@@ -179,6 +179,112 @@ def load_checkpoint(path, device):
         return torch.load(path, map_location=device, weights_only=True)
 
 
+def loss_sums(net, loader, criterion, device, shard=(0, 1)):
+    """Sum of per-batch mean loss x batch size over `loader` (the reference's
+    `loss += loss_.item() * len(y)`, methods/csghmc.py:620-627), accumulated
+    on the device in float64 — the same float64 operations in the same order,
+    without a host synchronisation per batch.  shard=(r, k): only batches
+    whose index is r mod k are scored.  Returns (device float64 sum, count)."""
+    r, k = shard
+    acc = torch.zeros((), dtype=torch.float64, device=device)
+    nb = 0
+    for i, (x, y) in enumerate(loader):
+        if i % k != r:
+            continue
+        x, y = x.to(device), y.to(device)
+        acc = add_loss(acc, criterion(net(x), y), len(y))
+        nb += len(y)
+    return acc, nb
+
+
+def _group_rank_size(group):
+    import torch.distributed as dist
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+def _check_same_posterior(group, device, *vecs):
+    """Sharded scoring needs the same Gaussian on every rank of the group:
+    compare float64 checksums (all_reduce MIN and MAX); raise if they differ."""
+    cs = torch.stack([v.double().sum() if v is not None else torch.zeros((), dtype=torch.float64,
+                                                                         device=device)
+                      for v in vecs]).reshape(-1)
+    lo, hi = _reduce_in(cs.clone(), "min", group), _reduce_in(cs.clone(), "max", group)
+    if not torch.equal(lo, hi):
+        raise ValueError("full_batch_likelihoods(group=...): the ranks of the group hold different "
+                         "posterior moments; a sharded pass needs the same mean / variance on every "
+                         "rank (replicas of one chain, or chains.pool_moments)")
+
+
+def _reduce_in(t, op, group):
+    import torch.distributed as dist
+    o = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op]
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=o, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=o, group=group)
+    return t
+
+
+def full_batch_likelihoods(runner, train_loader, mean, m2, var_mode, ratio, theta, group=None):
+    """methods/csghmc.py:568-638 (csgld.py:508-594, adam_csghmc.py:629-...):
+    max(1, nst) posterior draws theta_s = mean + sqrt(var) * eps (one fused
+    kernel each; nst = 0: the current theta), each scored on the full
+    training set; returns [exp(-average loss)] per draw.
+
+    group (a torch.distributed process group, or dist.group.WORLD): a
+    data-parallel pass — every rank of the group draws the SAME samples (the
+    group's first rank's Philox key; the moments must agree, checked) and
+    scores only the batches whose index is its group rank mod the group size;
+    ONE all_reduce of the [draws, 2] float64 (loss sum, count) table combines
+    them.  The loss sums equal the single-process ones up to the float64
+    summation order."""
+    import torch.distributed as dist
+    device = runner.args.device
+    model = runner.model
+    seed, chain = model.seed, model.chain
+    shard = (0, 1)
+    if group is not None:
+        if model.noise_mode != "philox":
+            raise ValueError("a sharded likelihood pass needs noise_mode='philox' (the draws must "
+                             "be a function of the group's common key)")
+        shard = _group_rank_size(group)
+        _check_same_posterior(group, mean.device, mean, m2)
+        key = torch.tensor([seed & ((1 << 63) - 1), chain], dtype=torch.int64,
+                           device=mean.device)
+        src = dist.get_global_rank(group, 0) if group is not dist.group.WORLD else 0
+        if key.is_cuda and dist.get_backend(group) == "gloo":
+            h = key.cpu()
+            dist.broadcast(h, src=src, group=group)
+            key.copy_(h)
+        else:
+            dist.broadcast(key, src=src, group=group)
+        seed, chain = int(key[0]), int(key[1])
+    draw = PosteriorDraw(runner.net, model.noise_mode, seed, chain, model.noise_provider)
+    ndraw = max(1, runner.nst)
+    table = torch.zeros(ndraw, 2, dtype=torch.float64, device=mean.device)
+    draw.net.eval()
+    with torch.no_grad():
+        for s in range(ndraw):
+            if runner.nst > 0:
+                draw.draw(mean, m2, var_mode, ratio)
+            else:
+                draw.theta.copy_(theta)
+            acc, nb = loss_sums(draw.net, train_loader, runner.criterion, device, shard)
+            table[s, 0] = acc
+            table[s, 1] = nb
+    if group is not None:
+        _reduce_in(table, "sum", group)
+    out = []
+    for s, (tot, nb) in enumerate(table.tolist()):
+        avg = tot / nb
+        out.append(np.exp(-avg))
+        runner.logger.info(f"Sample {s + 1} - Full batch average loss: {avg:.6f}, "
+                           f"likelihood: {np.exp(-avg):.6e}")
+    return out
+
+
 def gmm_weights(cycle_likelihoods):
     """methods/csghmc.py:641-670: w_c = 1 / mean(1/lik), normalised."""
     if not cycle_likelihoods:
@@ -194,8 +300,14 @@ def mixture_evaluate(runner, test_loader, var_of_cycle):
     """Cyclical methods' GMM predictive (methods/csghmc.py:387-514,
     methods/csgld.py:337-452).  var_of_cycle(c) -> (m2, var_mode, ratio)."""
     args = runner.args
-    weights = runner.calculate_gmm_weights()
-    runner.logger.info(f"GMM component weights: {weights}")
+    chain_w = None
+    if chain_world() > 1 and getattr(runner, "gmm_over_chains", False):
+        # the ensemble's components are every chain's cycles, weighted jointly
+        weights, chain_w, joint = chains.chain_gmm_weights(runner.cycle_likelihoods)
+        runner.logger.info(f"GMM component weights over chains: {joint}")
+    else:
+        weights = runner.calculate_gmm_weights()
+        runner.logger.info(f"GMM component weights: {weights}")
     model = runner.model
     draw = PosteriorDraw(runner.net, model.noise_mode, model.seed, model.chain,
                          model.noise_provider)
@@ -232,7 +344,8 @@ def mixture_evaluate(runner, test_loader, var_of_cycle):
                 (x.size(0), args.num_classes, 1, 1), device=x.device)
             if batch_logits is None:  # no cycle collected yet
                 batch_logits = draw.net(x)
-            batch_logits = chain_average_logprob(batch_logits) if chain_world() > 1 else batch_logits
+            if chain_world() > 1:
+                batch_logits = chains.average_predictive(batch_logits, chain_w)
             lb = runner.criterion(batch_logits, y)
             pred = batch_logits.data.max(dim=1)[1]
             targets.append(y.cpu().numpy())

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -74,21 +75,62 @@ def chain_seed(base_seed):
     return int(base_seed) + rank()
 
 
-def average_predictive(scores):
-    """Ensemble predictive over the K chains: log((1/K) sum_k softmax(s_k)),
-    per class.  Each chain's scores are normalised first (log_softmax: the
-    csghmc mixture's weighted logits are not log-probabilities, and chains may
-    differ in logit scale), then a max-shifted log-mean-exp over ranks — no
-    overflow for large logits, no -inf for classes every chain finds unlikely.
-    One process: the scores are returned unchanged (the reference's
-    single-chain evaluation)."""
+def average_predictive(scores, weight=None):
+    """Ensemble predictive over the K chains: log(sum_k w_k softmax(s_k)), per
+    class, with w_k = 1/K (weight=None) or this chain's weight (weights summing
+    to 1 over the chains, e.g. chain_gmm_weights).  Each chain's scores are
+    normalised first (log_softmax: the csghmc mixture's weighted logits are
+    not log-probabilities, and chains may differ in logit scale), then a
+    max-shifted log-sum-exp over ranks — no overflow for large logits, no -inf
+    for classes every chain finds unlikely.  One process: the scores are
+    returned unchanged (the reference's single-chain evaluation)."""
     k = world()
     if k == 1:
         return scores
     lp = torch.log_softmax(scores.float(), dim=1)
+    if weight is not None:
+        if weight <= 0:  # this chain contributes nothing; exp(-inf) = 0 below
+            lp = torch.full_like(lp, float("-inf"))
+        else:
+            lp = lp + float(np.log(weight))
     shift = _all_reduce(lp.clone(), dist.ReduceOp.MAX)
     s = _all_reduce_sum((lp - shift).exp())
-    return shift + (s / k).log()
+    return shift + (s if weight is not None else s / k).log()
+
+
+def gather_objects(obj):
+    """all_gather of a small picklable host object (one per rank, rank order)."""
+    if world() == 1:
+        return [obj]
+    out = [None] * world()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def chain_gmm_weights(cycle_likelihoods):
+    """calculate_gmm_weights over chains: the reference's
+    per-cycle weight w_c = 1 / mean(1 / lik) (methods/csghmc.py:641-670),
+    computed for every (chain, cycle) component of the ensemble and
+    normalised jointly — a chain whose cycles explain the training data better
+    weighs more in the ensemble predictive.  One all_gather of the chains'
+    likelihood lists (a few floats each).  Returns (within, chain_w, joint):
+    this chain's cycle weights normalised within the chain (what its own
+    mixture uses), this chain's total weight W_k (sum over its cycles, the
+    weight for average_predictive), and {(rank, cycle): w} for all chains."""
+    mine = {int(c): [float(v) for v in np.atleast_1d(lk)] for c, lk in cycle_likelihoods.items()}
+    every = gather_objects(mine)
+    raw = {(r, c): 1.0 / np.mean([1.0 / v for v in liks])
+           for r, d in enumerate(every) for c, liks in d.items()}
+    tot = sum(raw.values())
+    if not raw or not tot > 0:  # no cycle scored anywhere: uniform over chains
+        joint = {k: 1.0 / len(raw) for k in raw} if raw else {}
+        return ({c: 1.0 / len(mine) for c in mine} if mine else {0: 1.0}), 1.0 / world(), joint
+    joint = {k: v / tot for k, v in raw.items()}
+    r = rank()
+    chain_w = sum(v for (rr, _), v in joint.items() if rr == r)
+    within = {c: (joint[(r, c)] / chain_w if chain_w > 0 else 1.0 / len(mine)) for c in mine} \
+        if mine else {0: 1.0}
+    return within, chain_w, joint
 
 
 def gather_logits(logits_all):

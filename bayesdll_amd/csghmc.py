@@ -36,6 +36,10 @@ class Runner:
         self.args = R.bind_chain_log_dir(args)
         self.diverged_epochs = []
         self.logger = logger
+        # beyond the reference: a process group for a
+        # data-parallel likelihood pass, and GMM weights over the chains
+        self.likelihood_group = None
+        self.gmm_over_chains = bool(getattr(args, "gmm_over_chains", False))
         # prior backbone (zeros if not pretrained) — kept for API parity; the
         # cSGHMC update never reads it (Q1, methods/csghmc.py:759-762)
         if args.pretrained is None:
@@ -290,34 +294,17 @@ class Runner:
             self._cycle_completed(self.current_cycle)
         return ckpt["epoch"]
 
-    def full_batch_likelihoods(self, train_loader):
+    def full_batch_likelihoods(self, train_loader, group=None):
         """methods/csghmc.py:568-638: nst draws from the current cycle's
-        Gaussian, each scored on the full training set; returns exp(-loss)."""
+        Gaussian, each scored on the full training set; returns exp(-loss).
+        group (or self.likelihood_group): a data-parallel pass over the
+        group's ranks, one all-reduce of the loss sums (_runner)."""
         c = self.current_cycle
-        mean = self.cycle_theta_mom1[c]
         m2, var_mode, ratio = self._variance_source(c)
-        model = self.model
-        draw = R.PosteriorDraw(self.net, model.noise_mode, model.seed, model.chain,
-                               model.noise_provider)
-        likelihoods = []
-        for sample_idx in range(max(1, self.nst)):
-            if self.nst > 0:
-                draw.draw(mean, m2, var_mode, ratio)
-            else:
-                draw.theta.copy_(model.state_for(self.net).theta)
-            draw.net.eval()
-            loss, nb = 0.0, 0
-            with torch.no_grad():
-                for x, y in train_loader:
-                    x, y = x.to(self.args.device), y.to(self.args.device)
-                    lo = self.criterion(draw.net(x), y)
-                    loss += lo.item() * len(y)
-                    nb += len(y)
-            avg = loss / nb
-            likelihoods.append(np.exp(-avg))
-            self.logger.info(f"Sample {sample_idx + 1} - Full batch average loss: {avg:.6f}, "
-                             f"likelihood: {np.exp(-avg):.6e}")
-        return likelihoods
+        return R.full_batch_likelihoods(self, train_loader, self.cycle_theta_mom1[c], m2,
+                                        var_mode, ratio, self.model.state_for(self.net).theta,
+                                        group=group if group is not None else
+                                        self.likelihood_group)
 
     def calculate_gmm_weights(self):
         return R.gmm_weights(self.cycle_likelihoods)

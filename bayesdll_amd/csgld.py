@@ -36,6 +36,10 @@ class Runner:
         self.args = R.bind_chain_log_dir(args)
         self.diverged_epochs = []
         self.logger = logger
+        # beyond the reference: a process group for a
+        # data-parallel likelihood pass, and GMM weights over the chains
+        self.likelihood_group = None
+        self.gmm_over_chains = bool(getattr(args, "gmm_over_chains", False))
         if args.pretrained is None:
             self.net0 = copy.deepcopy(net)
             with torch.no_grad():
@@ -255,28 +259,14 @@ class Runner:
             self._cycle_completed(self.current_cycle)  # as csghmc.Runner.load_ckpt
         return ckpt["epoch"]
 
-    def full_batch_likelihoods(self, train_loader):
+    def full_batch_likelihoods(self, train_loader, group=None):
+        """methods/csgld.py:508-594 (as csghmc.Runner.full_batch_likelihoods)."""
         c = self.current_cycle
-        mean = self.cycle_theta_mom1[c]
         m2, mode, ratio = self._variance_source(c)
-        model = self.model
-        draw = R.PosteriorDraw(self.net, model.noise_mode, model.seed, model.chain,
-                               model.noise_provider)
-        out = []
-        for _ in range(max(1, self.nst)):
-            if self.nst > 0:
-                draw.draw(mean, m2, mode, ratio)
-            else:
-                draw.theta.copy_(self._state().theta)
-            draw.net.eval()
-            loss, nb = 0.0, 0
-            with torch.no_grad():
-                for x, y in train_loader:
-                    x, y = x.to(self.args.device), y.to(self.args.device)
-                    loss += self.criterion(draw.net(x), y).item() * len(y)
-                    nb += len(y)
-            out.append(np.exp(-loss / nb))
-        return out
+        return R.full_batch_likelihoods(self, train_loader, self.cycle_theta_mom1[c], m2, mode,
+                                        ratio, self._state().theta,
+                                        group=group if group is not None else
+                                        self.likelihood_group)
 
     def calculate_gmm_weights(self):
         return R.gmm_weights(self.cycle_likelihoods)

@@ -40,9 +40,13 @@ HPARAMS = {
 BASE_SEED = 77  # the same Philox seed on every chain: chains differ by chain id only
 
 
-def run_chain(method, chain=None):
+def run_chain(method, chain=None, replica=False):
     """Train + evaluate one chain on cuda (the current device).  chain=None:
-    the chain id is the process rank (bayesdll_amd.chains)."""
+    the chain id is the process rank (bayesdll_amd.chains).  replica=True
+    (cyclical methods, under torch.distributed): every rank runs the SAME
+    chain (chain id 0), then the cycle-end likelihood pass is run sharded
+    over the ranks and locally, the sharded pass is refused for ranks whose
+    moments differ, and evaluate() runs with GMM weights over chains."""
     import bayesdll_amd.csghmc as csghmc
     import bayesdll_amd.sgld as sgld
     dev = "cuda"
@@ -60,11 +64,33 @@ def run_chain(method, chain=None):
     runner = mod.Runner(net, None, args, logging.getLogger("chain"))
     if chain is not None:
         runner.model.chain = int(chain)
+    if replica:
+        runner.model.chain = 0
     runner.model.seed = BASE_SEED
     runner.train(train, None, test)
+    extra = {}
+    if method == "csghmc":
+        extra["lik_local"] = np.array(runner.full_batch_likelihoods(train))
+    if replica:
+        import torch.distributed as dist
+        from bayesdll_amd import chains
+        extra["lik_shard"] = np.array(runner.full_batch_likelihoods(train,
+                                                                    group=dist.group.WORLD))
+        c = runner.current_cycle
+        saved = runner.cycle_theta_mom1[c]
+        runner.cycle_theta_mom1[c] = saved + (1e-3 if chains.rank() == 1 else 0.0)
+        try:
+            runner.full_batch_likelihoods(train, group=dist.group.WORLD)
+            extra["mismatch_refused"] = np.bool_(False)
+        except ValueError:
+            extra["mismatch_refused"] = np.bool_(True)
+        runner.cycle_theta_mom1[c] = saved
+        runner.gmm_over_chains = True
+        extra["logits_gmm_over_chains"] = runner.evaluate(test)[3]
+        runner.gmm_over_chains = False
     loss, err, targets, logits, logits_all = runner.evaluate(test)
     torch.cuda.synchronize()
-    return {"log_dir": np.array(runner.args.log_dir),
+    return {**extra, "log_dir": np.array(runner.args.log_dir),
             "theta": runner.model.flat.theta.detach().cpu().numpy(),
             "chain": np.int64(runner.model.chain), "loss": np.float64(loss),
             "err": np.float64(err), "targets": targets, "logits": logits,
@@ -75,11 +101,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--method", required=True, choices=sorted(HPARAMS))
     ap.add_argument("--out", required=True)
+    ap.add_argument("--replica", action="store_true")
     a = ap.parse_args()
     from bayesdll_amd import chains
     chains.init_chains(backend="gloo")  # ranks share one GPU here; RCCL needs one GPU per rank
     try:
-        res = run_chain(a.method)
+        res = run_chain(a.method, replica=a.replica)
     finally:
         import torch.distributed as dist
         if dist.is_initialized():

@@ -39,7 +39,7 @@ def _free_port():
     return port
 
 
-def _run_ranks(method, tmp_path):
+def _run_ranks(method, tmp_path, extra=()):
     port = _free_port()
     procs, outs = [], []
     for r in range(WORLD):
@@ -47,7 +47,7 @@ def _run_ranks(method, tmp_path):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(WORLD),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "chain_worker.py"),
-                                       "--method", method, "--out", out], env=env,
+                                       "--method", method, "--out", out, *extra], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
         outs.append(out)
     logs = []
@@ -87,3 +87,25 @@ def test_two_chain_ensemble_matches_single_chains(method, tmp_path):
         np.testing.assert_allclose(ranks[r]["logits"], want, rtol=0, atol=2e-6)
     np.testing.assert_array_equal(ranks[0]["logits"], ranks[1]["logits"])
     assert ranks[0]["loss"] == ranks[1]["loss"] and ranks[0]["err"] == ranks[1]["err"]
+
+
+def test_sharded_likelihood_pass_and_gmm_weights_over_chains(tmp_path):
+    """SURVEY §8(f) row 3 through the product Runner: two ranks run the same
+    cSGHMC chain (replicas); the cycle-end full_batch_likelihoods sharded
+    over them (each scores half the training batches, one all-reduce of the
+    loss sums) equals the single-process pass (rtol 1e-6); ranks whose
+    moments differ are refused; evaluate() with GMM weights over chains gives
+    the single chain's predictive when the chains are identical."""
+    from chain_worker import run_chain
+    ranks = _run_ranks("csghmc", tmp_path, extra=("--replica",))
+    single = run_chain("csghmc", chain=0)
+    for r in range(WORLD):
+        np.testing.assert_array_equal(ranks[r]["theta"], single["theta"])
+        np.testing.assert_array_equal(ranks[r]["lik_local"], single["lik_local"])
+        assert len(ranks[r]["lik_shard"]) == 3  # nst draws
+        np.testing.assert_allclose(ranks[r]["lik_shard"], single["lik_local"], rtol=1e-6)
+        assert bool(ranks[r]["mismatch_refused"])
+        # identical chains: the jointly weighted ensemble is the chain's own mixture
+        np.testing.assert_allclose(ranks[r]["logits_gmm_over_chains"],
+                                   torch.log_softmax(torch.from_numpy(single["logits"]), 1).numpy(),
+                                   rtol=1e-5, atol=1e-5)
