@@ -31,6 +31,31 @@ from . import _lib as L
 from .flat import FlatState
 
 NOISE_MODES = ("philox", "torch", "external")
+
+# Captured graphs whose sampler was dropped while a capture was in progress on
+# this thread: destroying them then would free their private pools on a
+# capturing stream (a process abort), so they are parked here and destroyed at
+# the next point outside any capture (release_deferred_graphs).
+_DEFERRED_GRAPHS = []
+
+
+def release_deferred_graphs():
+    """Destroy the graphs parked by a sampler dropped during a capture."""
+    if _DEFERRED_GRAPHS and not torch.cuda.is_current_stream_capturing():
+        torch.cuda.synchronize()
+        _DEFERRED_GRAPHS.clear()
+
+
+def _drop_graphs(graphs):
+    """Destroy `graphs` (a list) now, or park them if a capture is running."""
+    if not graphs:
+        return
+    if torch.cuda.is_current_stream_capturing():
+        _DEFERRED_GRAPHS.extend(graphs)
+    else:
+        torch.cuda.synchronize()  # no replay of these graphs still in flight
+        graphs.clear()
+        release_deferred_graphs()
 MAX_GRAPHS = 4  # captured forward/backward graphs per sampler (one per input shape)
 
 
@@ -281,13 +306,22 @@ class FusedModelBase(nn.Module):
         call it when done with a sampler instead of leaving the graphs to the
         garbage collector."""
         graphs, self._graphs, self._graph_bound = self._graphs, {}, None
-        if graphs:
-            torch.cuda.synchronize()  # no replay of these graphs still in flight
-        graphs.clear()
+        _drop_graphs(list(graphs.values()))
+
+    def __del__(self):
+        """A dropped sampler releases its graphs deterministically here (or
+        parks them when dropped inside another capture), instead of leaving
+        their pools to whichever garbage collection runs next."""
+        try:
+            if getattr(self, "_graphs", None):
+                self.release_graphs()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
 
     def _capture(self, st, net, x, y, criterion):
         sx, sy = x.detach().clone(), y.detach().clone()
         gc.collect()  # pending garbage (old pools included) goes before the capture, not in it
+        release_deferred_graphs()
         # warm-up passes on a side stream (library handles, autotuned kernels)
         # must not move the network's state: keep buffers (BatchNorm running
         # statistics) and the device RNG as they were

@@ -135,6 +135,11 @@ def placed_vectors(n, device, names, method):
             runs_by_n[m] = build_runs([0], [m], [L.ATTR_PRIOR], m).to(device)
         return _placement_launcher(method, roles, m, device, runs_by_n[m])
 
+    from . import kernels as K
+    # placement launches run at their own depth (the kernels' <..., 2>
+    # instances), so a kernel-trace summary of the run's production kernel
+    # (depth 4 after autotuning) holds only full-size launches
+    prev = K.set_launch_config(1, 2, 1)
     try:
         vecs, info = P.place(n, device, names, launcher, lambda f: _time_launch(f, device, 3),
                              budget_bytes=int(0.25 * free), search=mode == "search")
@@ -144,6 +149,8 @@ def placed_vectors(n, device, names, method):
                       "using torch's allocator")
         return {nm: torch.zeros(n, **f32) for nm in names}, {"allocator": "torch",
                                                              "error": str(e)[:200]}
+    finally:
+        K.restore_launch_config(prev)
     info["method"] = method
     return vecs, info
 

@@ -270,6 +270,12 @@ def set_launch_config(blocks_per_cu=0, unroll=0, grid_stride=0):
     return L.lib().bdl_set_launch_config(int(blocks_per_cu), int(unroll), int(grid_stride))
 
 
+def restore_launch_config(packed):
+    """Re-install the geometry a set_launch_config call returned (packed as
+    (grid_stride << 24) | (blocks_per_cu << 8) | unroll)."""
+    return set_launch_config((packed >> 8) & 0xFFFF, packed & 0xFF, (packed >> 24) & 0xFF)
+
+
 def _use_geometry(state):
     """Install the geometry tuned for this state's size (state.launch_cfg, set
     from autotune_once) if another state's is active: the library's launch

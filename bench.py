@@ -545,12 +545,19 @@ def main():
                      "traffic": traffic,
                      # not this run's counters: rocprofv3 PMC (FETCH/WRITE_SIZE passes) of the
                      # same kernel on the same workload, per launch, committed under profiles/
+                     "traffic_kind": "profile (committed rocprofv3 PMC passes, not this run)",
                      "traffic_source": (f"{os.path.relpath(a.traffic, ROOT)}[{a.backbone}][{dominant}]"
                                         if traffic is not None else None),
                      "alg_bytes_per_launch": alg_bytes},
     }
     if not a.no_aux:
         out["aux_kernels"] = aux_kernels(st)
+        try:  # HBM bytes per launch of the same sweeps from the committed PMC profile
+            tj = json.load(open(a.traffic))
+            for k, v in out["aux_kernels"].items():
+                v["traffic"] = tj.get(a.backbone, {}).get(k)
+        except Exception:  # noqa: BLE001
+            pass
     if world == 1 and a.e2e_steps > 0 and a.backbone == "vit_l_32" and not sgld:
         del st, m1s, m2s
         torch.cuda.empty_cache()

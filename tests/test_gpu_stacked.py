@@ -447,6 +447,36 @@ def test_graph_capture_with_pending_garbage():
     assert not during_capture, during_capture
 
 
+def test_sampler_dropped_inside_a_capture_parks_its_graphs():
+    """A graph-mode sampler whose last reference goes while ANOTHER capture is
+    running (user code capturing its own graph) must not destroy its graphs
+    there (their pools would be freed on a capturing stream): Model.__del__
+    parks them (_base._DEFERRED_GRAPHS) and they are destroyed at the next
+    point outside any capture."""
+    import weakref
+    import bayesdll_amd.csghmc as csghmc
+    from bayesdll_amd import _base
+    x = torch.randn(8, 13, device="cuda")
+    y = torch.randint(0, 5, (8,), device="cuda")
+    net = Net().cuda()
+    model = csghmc.Model(100.0, prior_sig=1.0, momentum_decay=0.1)
+    model.graph = True
+    model(x, y, net, None, torch.nn.CrossEntropyLoss(), [1e-3, 1e-3], 1.0, 1.0)
+    assert model.graph_captures == 1 and len(model._graphs) == 1
+    gref = weakref.ref(next(iter(model._graphs.values()))["graph"])
+    z = torch.zeros(4, device="cuda")
+    user = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(user):
+        z.add_(1.0)
+        del model  # the sampler goes mid-capture
+        assert len(_base._DEFERRED_GRAPHS) == 1 and gref() is not None
+    user.replay()
+    _base.release_deferred_graphs()
+    assert not _base._DEFERRED_GRAPHS and gref() is None
+    torch.cuda.synchronize()
+    assert z.tolist() == [1.0] * 4
+
+
 def test_stacked_refuses_batchnorm_statistics():
     from bayesdll_amd import stacked
     net = nn.Sequential(nn.Linear(4, 4), nn.BatchNorm1d(4)).cuda()
