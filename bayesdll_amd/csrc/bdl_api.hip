@@ -971,12 +971,17 @@ int bdl_vmm_map(int32_t device, const uint64_t* handles, int32_t nchunks, uint64
   return rc;
 }
 
+// The virtual range stays RESERVED after the unmap, for the life of the
+// process: a range freed with hipMemAddressFree is handed out again by the next
+// reservation, and on this stack the GPU then keeps translating it to the
+// PREVIOUS mapping's physical chunks for a while — writes through the new
+// mapping land in the old (possibly released) memory (tools/vmm_alias_check.py,
+// profiles/round2/vmm/alias_reuse.jsonl).  Never reusing a range costs only
+// virtual address space (a chain state reserves a few tens of GB of it).
 int bdl_vmm_unmap(void* va, uint64_t total_bytes) {
   if (!va) return fail(BDL_ERR_NULL, "bdl_vmm_unmap: null va");
-  hipError_t e = hipMemUnmap(va, total_bytes);
+  const hipError_t e = hipMemUnmap(va, total_bytes);
   if (e != hipSuccess) return hip_fail("bdl_vmm_unmap: hipMemUnmap", e);
-  e = hipMemAddressFree(va, total_bytes);
-  if (e != hipSuccess) return hip_fail("bdl_vmm_unmap: hipMemAddressFree", e);
   return BDL_OK;
 }
 

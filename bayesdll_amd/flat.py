@@ -141,7 +141,7 @@ def placed_vectors(n, device, names, method):
     # (depth 4 after autotuning) holds only full-size launches
     prev = K.set_launch_config(1, 2, 1)
     try:
-        vecs, info = P.place(n, device, names, launcher, lambda f: _time_launch(f, device, 3),
+        vecs, info = P.place(n, device, names, launcher, lambda f: _time_launch(f, device, 5),
                              budget_bytes=int(0.25 * free), search=mode == "search")
     except RuntimeError as e:  # chunk mappings unavailable: plain allocations
         import warnings

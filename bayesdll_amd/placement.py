@@ -17,13 +17,18 @@ into one virtual range (hipMemMap), so the pairing is chosen chunk by chunk:
   2. time the method's production kernel on every ordered chunk pair
      (theta = chunk i, momentum = chunk j, the other roles on further
      chunks) — chunk-sized sweeps, a few launches each;
-  3. greedily take the fastest disjoint (i, j) pairs for theta / momentum,
-     the other roles get the remaining chunks in allocation order; if the
-     pair times show no spread, allocate more spares (bounded) first;
-  4. map the composite vectors; time the chosen assignment and the
-     allocation-order one at full size, keep the faster; unmap the per-chunk
-     views and release every handle (unchosen chunks return to the driver at
-     once — nothing is parked in torch's cache).
+  3. if the pair times show no clearly fast pair, allocate more spares
+     (bounded) first;
+  4. candidate assignments: the allocation order, up to COMPOSITES
+     greedy ones (seeded by each of the fastest pairs, completed with the
+     fastest disjoint pairs; theta / momentum from the pairs, the other roles
+     from the remaining chunks in allocation order); each is mapped and timed
+     at FULL size — chunk-pair times only rank the seeds; and, competing
+     with them, the roles allocated plainly by torch with TORCH_PAIRINGS
+     (theta, mom) pairings among those allocations (on some boxes hipMalloc'd
+     memory pairs faster than any chunk composite).  The fastest is kept; the per-chunk views are unmapped and every handle released
+     (unchosen chunks return to the driver at once — nothing is parked in
+     torch's cache).
 
 Results never depend on placement (the kernels read the same values from any
 address).  The mapped ranges are exposed to torch through
@@ -33,6 +38,7 @@ capture (it is then queued and unmapped at the next release point)."""
 from __future__ import annotations
 
 import ctypes as C
+import itertools
 import math
 
 import torch
@@ -43,6 +49,8 @@ CHUNK_TARGET = 1 << 30   # chunk size bound: vectors of up to 1 GiB are one chun
 ALIGN = 2 << 20          # chunk sizes are multiples of 2 MiB (large-page mappings)
 FAST_PAIR = 0.97         # a pair this much faster than the median pair is worth taking
 SPARE_ROUNDS = 2         # at most this many rounds of extra chunks while none is seen
+COMPOSITES = 6           # full-size candidate assignments timed besides allocation order
+TORCH_PAIRINGS = 3       # (theta, mom) pairings tried among plain torch allocations
 
 _pending = []  # (device index, va, total bytes) whose unmap was deferred (graph capture)
 
@@ -141,7 +149,8 @@ def _has_fast_pair(times):
     return t[0] < FAST_PAIR * t[len(t) // 2]
 
 
-def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, search=True):
+def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, search=True,
+          with_torch=True):
     """Allocate `names` (fp32, n elements each, zeroed) from physical chunks,
     theta / mom paired fast.  `launcher(roles: {name: tensor}, n)` returns a
     zero-argument launch of the sampler's kernel; `time_launch(launch)` its
@@ -186,55 +195,101 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
             ch.add(spare)
             rounds += 1
 
-        # greedy disjoint (theta, mom) pairs, fastest first
-        used, th_ids, mom_ids = set(), [], []
-        for (i, j), _t in sorted(times.items(), key=lambda kv: kv[1]):
-            if i in used or j in used:
-                continue
-            th_ids.append(i)
-            mom_ids.append(j)
-            used.update((i, j))
-            if len(th_ids) == per:
-                break
-        rest = [k for k in range(len(ch.views)) if k not in used]
+        ranked = sorted(times, key=times.get)
+
+        def greedy(first):
+            """Disjoint (theta, mom) chunk pairs: `first`, then the fastest
+            remaining ones."""
+            used, th, mo = set(), [], []
+            for i, j in [first] + ranked:
+                if i in used or j in used:
+                    continue
+                th.append(i)
+                mo.append(j)
+                used.update((i, j))
+                if len(th) == per:
+                    break
+            rest = [k for k in range(len(ch.views)) if k not in used]
+            out, r = {}, 0
+            for q, nm in enumerate(names):
+                if q == it:
+                    out[nm] = th
+                elif q == im:
+                    out[nm] = mo
+                else:
+                    out[nm] = rest[r * per:(r + 1) * per]
+                    r += 1
+            return out
 
         def composite(assign):
             return {nm: Mapping(dev_index, [ch.handles[k] for k in ids], cb, n).tensor()
                     for nm, ids in assign.items()}
 
-        chosen, r = {}, 0
-        for q, nm in enumerate(names):
-            if q == it:
-                chosen[nm] = th_ids
-            elif q == im:
-                chosen[nm] = mom_ids
-            else:
-                chosen[nm] = rest[r * per:(r + 1) * per]
-                r += 1
+        # candidates: allocation order, then greedy completions seeded by the
+        # fastest distinct pairs — each timed at FULL size (the chunk-pair
+        # times only rank the seeds: they predict a composite weakly)
         default = {nm: list(range(q * per, (q + 1) * per)) for q, nm in enumerate(names)}
-        if not search:
-            chosen = default
-        vec_c = composite(chosen)
-        vec_d = composite(default) if search else vec_c
-        for v in list(vec_c.values()) + list(vec_d.values()):
-            v.zero_()
-        ms_c = time_launch(launcher(vec_c, n))
-        ms_d = time_launch(launcher(vec_d, n)) if search else ms_c
-        keep, drop = (vec_c, vec_d) if ms_c <= ms_d else (vec_d, vec_c)
+        cands = [default]
+        for first in ranked:
+            if len(cands) > COMPOSITES:
+                break
+            c = greedy(first)
+            if c not in cands:
+                cands.append(c)
+        best, best_ms, comp_ms, best_src = None, None, [], None
+        for c in cands:
+            vec = composite(c)
+            for v in vec.values():
+                v.zero_()
+            ms = time_launch(launcher(vec, n))
+            comp_ms.append(round(ms, 4))
+            if best_ms is None or ms < best_ms:
+                best, best_ms, chosen, best_src = vec, ms, c, "chunks"
+            del vec
+        ms_d = comp_ms[0]
+        # torch's own allocations compete too (on some boxes hipMalloc'd
+        # memory pairs faster than any chunk composite): the roles' vectors
+        # allocated plainly, with every (theta, mom) pairing among them
+        torch_ms = []
+        if search and with_torch:
+            tv = [torch.zeros(n, dtype=torch.float32, device=device) for _ in names]
+            pairs = [(it, im)] + [p for p in itertools.combinations(range(len(tv)), 2)
+                                  if set(p) != {it, im}]
+            for i, j in pairs[:TORCH_PAIRINGS]:
+                rest = [k for k in range(len(tv)) if k not in (i, j)]
+                vec, r = {}, 0
+                for q, nm in enumerate(names):
+                    if q == it:
+                        vec[nm] = tv[i]
+                    elif q == im:
+                        vec[nm] = tv[j]
+                    else:
+                        vec[nm] = tv[rest[r]]
+                        r += 1
+                ms = time_launch(launcher(vec, n))
+                torch_ms.append(round(ms, 4))
+                if ms < best_ms:
+                    best, best_ms, best_src = vec, ms, "torch"
+                    chosen = {nm: [] for nm in names}
+            del tv
+        keep = best
         for v in keep.values():
             v.zero_()
-        del drop, vec_c, vec_d
+        th_ids, mom_ids = chosen[names[it]], chosen[names[im]]
         nk = len(ch.views)
     finally:
         ch.release()
     pair_ms = sorted(times.values()) or [float("nan")]
-    info = {"allocator": "vmm", "search": bool(search), "chunk_mb": cb >> 20,
+    info = {"allocator": "torch" if best_src == "torch" else "vmm", "search": bool(search), "chunk_mb": cb >> 20,
             "chunks_per_vector": per, "chunks_allocated": nk,
             "pairs_timed": len(times), "pair_ms_min": round(pair_ms[0], 4),
             "pair_ms_median": round(pair_ms[len(pair_ms) // 2], 4),
             "pair_ms_max": round(pair_ms[-1], 4),
             "seconds": round(time.perf_counter() - t_start, 3),
-            "default_ms": round(ms_d, 4), "chosen_ms": round(min(ms_c, ms_d), 4),
-            "kept": "chosen" if ms_c <= ms_d else "default",
+            "default_ms": ms_d, "chosen_ms": round(best_ms, 4),
+            "untuned_torch_ms": torch_ms[0] if torch_ms else None,
+            "composites_ms": comp_ms, "torch_ms": torch_ms,
+            "kept": best_src if best_src == "torch" else
+            ("default" if chosen is cands[0] else "search"),
             "theta_chunks": th_ids, "mom_chunks": mom_ids}
     return keep, info

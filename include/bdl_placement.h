@@ -42,7 +42,11 @@ int bdl_chunk_release(uint64_t handle);
 int bdl_vmm_map(int32_t device, const uint64_t* handles, int32_t nchunks, uint64_t chunk_bytes,
                 void** va);
 
-/* Unmap and free a range returned by bdl_vmm_map (total = nchunks * chunk_bytes). */
+/* Unmap a range returned by bdl_vmm_map (total = nchunks * chunk_bytes); its
+ * physical chunks are freed once unmapped everywhere and released.  The
+ * virtual range itself stays reserved for the life of the process: a range
+ * handed out again is translated to the old mapping's memory for a while on
+ * this driver stack (measured), so ranges are never reused. */
 int bdl_vmm_unmap(void* va, uint64_t total_bytes);
 
 #ifdef __cplusplus
