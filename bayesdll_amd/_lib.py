@@ -23,6 +23,7 @@ NOISE_NONE, NOISE_BUFFER, NOISE_PHILOX = 0, 1, 2
 COLLECT_NONE, COLLECT_WELFORD_INIT, COLLECT_WELFORD, COLLECT_MEAN_INIT, COLLECT_MEAN = range(5)
 ATTR_HEAD, ATTR_PRIOR, ATTR_SKIP, ATTR_GUNALIGNED = 0x1, 0x2, 0x4, 0x8
 FLAG_FIRST_STEP, FLAG_RECIP_DIV, FLAG_MOMENTUM, FLAG_GRAD_READY = 0x1, 0x2, 0x4, 0x8
+FLAG_PLACEMENT_PROBE = 0x10
 VAR_GIVEN, VAR_RAW_MOMENTS, VAR_WELFORD = 0, 1, 2
 ABI_VERSION = 6
 

@@ -460,6 +460,26 @@ StepKernel pick_step(int method, int noise, int collect, int unroll) {
   return nullptr;
 }
 
+// Placement probe (BDL_FLAG_PLACEMENT_PROBE): the production update under its
+// own symbol, so that the buffer-placement timing launches (flat.placed_vectors)
+// never mix into a kernel-trace summary of the production kernels.
+template <int METHOD, int NOISE, int COLLECT, int UNROLL>
+__global__ __launch_bounds__(kBlock) void bdl_probe_kernel(const KArgs a) {
+  if (a.flags & BDL_FLAG_RECIP_DIV)
+    step_body<METHOD, NOISE, COLLECT, true, UNROLL>(a);
+  else
+    step_body<METHOD, NOISE, COLLECT, false, UNROLL>(a);
+}
+
+StepKernel pick_probe(int method, int noise, int collect) {
+  if (collect != BDL_COLLECT_NONE) return nullptr;
+  if (method == BDL_CSGHMC && noise == BDL_NOISE_NONE)
+    return bdl_probe_kernel<BDL_CSGHMC, BDL_NOISE_NONE, BDL_COLLECT_NONE, 4>;
+  if (method == BDL_SGLD && noise == BDL_NOISE_PHILOX)
+    return bdl_probe_kernel<BDL_SGLD, BDL_NOISE_PHILOX, BDL_COLLECT_NONE, 4>;
+  return nullptr;
+}
+
 int grid_for(int64_t ngroups, int per_block_groups) {
   const int64_t want = (ngroups + per_block_groups - 1) / per_block_groups;
   const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
@@ -532,8 +552,10 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   for (const void* p : ptrs)
     if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_sgmcmc_step: vector not 16-B aligned");
 
-  const int unroll = g_unroll;
-  StepKernel k = pick_step(s->method, s->noise_mode, s->collect, unroll);
+  const bool probe = (s->flags & BDL_FLAG_PLACEMENT_PROBE) != 0;
+  const int unroll = probe ? 4 : g_unroll;
+  StepKernel k = probe ? pick_probe(s->method, s->noise_mode, s->collect)
+                       : pick_step(s->method, s->noise_mode, s->collect, unroll);
   if (!k) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: unsupported method/noise/collect combination");
 
   const int64_t ngroups = (s->n + 3) / 4;

@@ -74,26 +74,27 @@ PLACEMENT_MIN_ELEMS = 1 << 24  # below ~64 MB per vector placement effects are n
 
 
 def _placement_launcher(method, vs, n, device, runs):
-    """The sampler's production kernel on scratch vectors `vs` (role -> tensor)."""
+    """The sampler's update on scratch vectors `vs` (role -> tensor), launched
+    as the placement probe (BDL_FLAG_PLACEMENT_PROBE: the production update
+    under its own kernel symbol, so placement timing never mixes into a
+    kernel-trace summary of the production kernels).  cSGHMC: the explore
+    update (theta rw, grad r, mom rw); SGLD and the Adam variants: SGLD + SGD
+    momentum with Philox noise (theta rw, grad r, prior r, buffer rw — the
+    theta / buffer pairing placement optimises)."""
     from types import SimpleNamespace
 
     from . import kernels as K
     st = SimpleNamespace(theta=vs["theta"], grad=vs["grad"], mom=vs.get("mom"),
                          prior=vs.get("prior"), noise=None, runs=runs, nruns=1, n=n,
                          device=device)
-    if method == "adam" and "adam_m" in vs:
-        return lambda: K.adam_step(
-            st, L.ADAM_SGHMC, adam_m=vs["adam_m"], adam_v=vs["adam_v"],
-            sgd_buf=vs.get("sgd_buf"), beta1=0.9, beta2=0.999, eps=1e-8, t=3,
-            momentum_decay=0.1, nd=0.01, lrs=(1e-4, 1e-4), noise_mode=L.NOISE_PHILOX,
-            sigma2=1.0, n_data=1e6, mu=0.5, momentum="sgd_buf" in vs)
     if method == "csghmc":
         return lambda: K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-4, 1e-4), noise_scale=(0.0, 0.0),
-                                     noise_mode=L.NOISE_NONE, one_minus_alpha=0.9, prior_sig=1.0)
+                                     noise_mode=L.NOISE_NONE, one_minus_alpha=0.9, prior_sig=1.0,
+                                     probe=True)
     if method in ("sgld", "adam"):
         return lambda: K.sgmcmc_step(st, L.SGLD, lrs=(1e-4, 1e-4), noise_scale=(1e-3, 1e-3),
                                      noise_mode=L.NOISE_PHILOX, sigma2=1.0, n_data=1e6, mu=0.5,
-                                     momentum=st.mom is not None)
+                                     momentum=st.mom is not None, probe=True)
     raise ValueError(f"placed_vectors: unknown method {method!r}")
 
 
@@ -136,10 +137,9 @@ def placed_vectors(n, device, names, method):
         return _placement_launcher(method, roles, m, device, runs_by_n[m])
 
     from . import kernels as K
-    # placement launches run at their own depth (the kernels' <..., 2>
-    # instances), so a kernel-trace summary of the run's production kernel
-    # (depth 4 after autotuning) holds only full-size launches
-    prev = K.set_launch_config(1, 2, 1)
+    # one workgroup per CU for every placement timing (the probe kernel's depth
+    # is fixed at 4), whatever geometry another state installed
+    prev = K.set_launch_config(1, 4, 1)
     try:
         vecs, info = P.place(n, device, names, launcher, lambda f: _time_launch(f, device, 5),
                              budget_bytes=int(0.25 * free), search=mode == "search")

@@ -38,7 +38,7 @@ def _step_args(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1
                prior_sig=0.0, sigma2=1.0, n_data=1.0, mu=0.0, first_step=False,
                momentum=False, collect=L.COLLECT_NONE, mom1=None, mom2=None, collect_a=1.0,
                collect_b=1.0, seed=0, chain=0, step=0, div_mode=None, noise=None, grad_ready=False,
-               mom_buf=None, philox_offset=0):
+               mom_buf=None, philox_offset=0, probe=False):
     a = L.StepArgs()
     a.theta = state.theta.data_ptr()
     g = getattr(state, "grad", None)
@@ -60,7 +60,8 @@ def _step_args(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1
     a.noise_mode = int(noise_mode)
     a.collect = int(collect)
     a.flags = ((L.FLAG_FIRST_STEP if first_step else 0) | (L.FLAG_MOMENTUM if momentum else 0)
-               | (L.FLAG_GRAD_READY if grad_ready else 0) | _div_flag(div_mode))
+               | (L.FLAG_GRAD_READY if grad_ready else 0) | _div_flag(div_mode)
+               | (L.FLAG_PLACEMENT_PROBE if probe else 0))
     a.n = state.n
     a.lr[0], a.lr[1] = float(lrs[0]), float(lrs[1])
     a.noise_scale[0], a.noise_scale[1] = float(noise_scale[0]), float(noise_scale[1])

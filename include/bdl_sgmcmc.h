@@ -112,6 +112,11 @@ typedef enum bdl_collect {
 #define BDL_FLAG_MOMENTUM 0x4    /* SGD momentum != 0: maintain args.mom as SGD buffer */
 #define BDL_FLAG_GRAD_READY 0x8  /* BDL_SGLD/BDL_SGHMC: grad already holds the sampler gradient
                                     (e.g. clipped after a *_GRAD call): apply the SGD step only */
+#define BDL_FLAG_PLACEMENT_PROBE 0x10 /* the same update under a separate kernel symbol
+                                       * (bdl_probe_kernel, depth 4), so the timing launches of
+                                       * buffer placement stay out of profiles of the production
+                                       * kernels; BDL_COLLECT_NONE, and (BDL_CSGHMC, NOISE_NONE)
+                                       * or (BDL_SGLD, NOISE_PHILOX) only */
 
 /* One parameter tensor in named_parameters order (host input to bdl_build_runs). */
 typedef struct bdl_segment {

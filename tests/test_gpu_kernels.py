@@ -674,6 +674,37 @@ def test_chunk_mapping_lifetime():
     del view
 
 
+def test_composites_mapped_one_after_another_do_not_alias():
+    """Placement maps and drops many composites of the same chunks.  A freed
+    virtual range handed out again was translated to the previous mapping's
+    chunks on this stack (tools/vmm_alias_check.py), so bdl_vmm_unmap keeps
+    ranges reserved: every composite must write exactly its own chunks and
+    get a range no earlier mapping had."""
+    import random
+    from bayesdll_amd import placement as P
+    cb = 64 << 20
+    ch = P._Chunks(0, cb)
+    ch.add(6)
+    try:
+        rng = random.Random(3)
+        seen = set()
+        for _ in range(8):
+            ids = rng.sample(range(6), 4)
+            a = P.Mapping(0, [ch.handles[k] for k in ids[:2]], cb, 2 * cb // 4).tensor()
+            b = P.Mapping(0, [ch.handles[k] for k in ids[2:]], cb, 2 * cb // 4).tensor()
+            assert a.data_ptr() not in seen and b.data_ptr() not in seen
+            seen.update((a.data_ptr(), b.data_ptr()))
+            a.fill_(1.0)
+            b.fill_(2.0)
+            torch.cuda.synchronize()
+            for k, want in zip(ids, (1.0, 1.0, 2.0, 2.0)):
+                v = ch.views[k]
+                assert float(v.min()) == want and float(v.max()) == want, (ids, k)
+            del a, b
+    finally:
+        ch.release()
+
+
 def test_full_size_vit_csghmc_sample_and_welford_collect_bitexact():
     """The headline schedule's sample steps at full ViT-L/32 size: Philox noise
     + Welford first sample (m1 = theta, M2 = 0) then a Welford update with the
