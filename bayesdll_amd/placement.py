@@ -149,6 +149,49 @@ def _has_fast_pair(times):
     return t[0] < FAST_PAIR * t[len(t) // 2]
 
 
+def candidate_assignments(times, nchunks, names, per, limit=COMPOSITES):
+    """Chunk ids per role for the full-size candidates: the allocation order
+    first, then up to `limit` greedy assignments — each seeded by one of the
+    fastest (theta, mom) chunk pairs of `times` ({(i, j): ms}) and completed
+    with the fastest pairs disjoint from it; theta / mom take the pairs' chunks,
+    the other roles the remaining chunks in allocation order.  Chunk-pair
+    times only rank the seeds (they predict a composite weakly), so every
+    candidate is timed at full size afterwards.  No chunk serves two roles."""
+    it, im = names.index("theta"), names.index("mom")
+    ranked = sorted(times, key=times.get)
+
+    def greedy(first):
+        used, th, mo = set(), [], []
+        for i, j in [first] + ranked:
+            if i in used or j in used:
+                continue
+            th.append(i)
+            mo.append(j)
+            used.update((i, j))
+            if len(th) == per:
+                break
+        rest = [k for k in range(nchunks) if k not in used]
+        out, r = {}, 0
+        for q, nm in enumerate(names):
+            if q == it:
+                out[nm] = th
+            elif q == im:
+                out[nm] = mo
+            else:
+                out[nm] = rest[r * per:(r + 1) * per]
+                r += 1
+        return out
+
+    cands = [{nm: list(range(q * per, (q + 1) * per)) for q, nm in enumerate(names)}]
+    for first in ranked:
+        if len(cands) > limit:
+            break
+        c = greedy(first)
+        if c not in cands:
+            cands.append(c)
+    return cands
+
+
 def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, search=True,
           with_torch=True):
     """Allocate `names` (fp32, n elements each, zeroed) from physical chunks,
@@ -195,47 +238,11 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
             ch.add(spare)
             rounds += 1
 
-        ranked = sorted(times, key=times.get)
-
-        def greedy(first):
-            """Disjoint (theta, mom) chunk pairs: `first`, then the fastest
-            remaining ones."""
-            used, th, mo = set(), [], []
-            for i, j in [first] + ranked:
-                if i in used or j in used:
-                    continue
-                th.append(i)
-                mo.append(j)
-                used.update((i, j))
-                if len(th) == per:
-                    break
-            rest = [k for k in range(len(ch.views)) if k not in used]
-            out, r = {}, 0
-            for q, nm in enumerate(names):
-                if q == it:
-                    out[nm] = th
-                elif q == im:
-                    out[nm] = mo
-                else:
-                    out[nm] = rest[r * per:(r + 1) * per]
-                    r += 1
-            return out
-
         def composite(assign):
             return {nm: Mapping(dev_index, [ch.handles[k] for k in ids], cb, n).tensor()
                     for nm, ids in assign.items()}
 
-        # candidates: allocation order, then greedy completions seeded by the
-        # fastest distinct pairs — each timed at FULL size (the chunk-pair
-        # times only rank the seeds: they predict a composite weakly)
-        default = {nm: list(range(q * per, (q + 1) * per)) for q, nm in enumerate(names)}
-        cands = [default]
-        for first in ranked:
-            if len(cands) > COMPOSITES:
-                break
-            c = greedy(first)
-            if c not in cands:
-                cands.append(c)
+        cands = candidate_assignments(times, len(ch.views), names, per)
         best, best_ms, comp_ms, best_src = None, None, [], None
         for c in cands:
             vec = composite(c)

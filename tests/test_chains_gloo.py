@@ -1,5 +1,6 @@
-"""Multi-chain logic on CPU with torch.distributed gloo, world_size 2 and 4
-(stands in for RCCL over xGMI: the same all_reduce / all_gather calls)."""
+"""Multi-chain logic on CPU with torch.distributed gloo, world_size 2, 4 and 8
+(stands in for RCCL over xGMI: the same all_reduce / all_gather calls; 8 = config
+5's chain count)."""
 import os
 import socket
 
@@ -48,7 +49,7 @@ def _worker(r, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_average_predictive_and_gather_chains(world):
     port = _free_port()
     ctx = mp.get_context("spawn")

@@ -1,0 +1,66 @@
+"""Host logic of the physical-chunk placement (bayesdll_amd.placement) — no GPU:
+chunk geometry and the candidate assignments the full-size timing chooses from
+(DESIGN.md §4 "Placement")."""
+import random
+
+import pytest
+
+from bayesdll_amd import placement as P
+
+
+@pytest.mark.parametrize("n", [1 << 24, 44549160, 306535400, 305548325, (1 << 28) + 1])
+def test_chunk_geometry_covers_the_vector_in_2mib_chunks_of_at_most_1gib(n):
+    per, cb = P.chunk_geometry(n)
+    assert cb % P.ALIGN == 0 and cb <= P.CHUNK_TARGET + P.ALIGN
+    assert per * cb >= 4 * n > (per - 1) * cb
+    assert per == -(-4 * n // P.CHUNK_TARGET)
+
+
+def test_vit_l_32_is_two_chunks_of_586_mib():
+    per, cb = P.chunk_geometry(306535400)
+    assert (per, cb >> 20) == (2, 586)
+
+
+@pytest.mark.parametrize("names", [["theta", "grad", "mom"],
+                                   ["theta", "grad", "mom", "prior"],
+                                   ["theta", "grad", "mom", "prior", "adam_m", "adam_v", "sgd_buf"]])
+@pytest.mark.parametrize("per", [1, 2, 3])
+def test_candidates_are_disjoint_role_assignments(names, per):
+    nchunks = len(names) * per + 2 * per
+    rng = random.Random(per * 31 + len(names))
+    times = {(i, j): rng.random() for i in range(nchunks) for j in range(nchunks) if i != j}
+    cands = P.candidate_assignments(times, nchunks, names, per)
+    # allocation order first
+    assert cands[0] == {nm: list(range(q * per, (q + 1) * per)) for q, nm in enumerate(names)}
+    assert 2 <= len(cands) <= P.COMPOSITES + 1
+    seen = []
+    for c in cands:
+        assert list(c) == names
+        ids = [k for nm in names for k in c[nm]]
+        assert all(len(c[nm]) == per for nm in names)
+        assert len(ids) == len(set(ids)) and all(0 <= k < nchunks for k in ids)
+        assert c not in seen
+        seen.append(c)
+    # the first greedy candidate holds the fastest pair as theta / mom chunk 0
+    best = min(times, key=times.get)
+    assert (cands[1]["theta"][0], cands[1]["mom"][0]) == best
+
+
+def test_greedy_completion_takes_the_fastest_disjoint_pairs():
+    names = ["theta", "grad", "mom"]
+    # chunk pairs (0, 1) and (2, 3) fastest; anything touching 0..3 otherwise slow
+    times = {(i, j): 1.0 for i in range(8) for j in range(8) if i != j}
+    times[(0, 1)] = 0.1
+    times[(2, 3)] = 0.2
+    times[(4, 5)] = 0.3
+    c = P.candidate_assignments(times, 8, names, 2)[1]
+    assert c["theta"] == [0, 2] and c["mom"] == [1, 3] and c["grad"] == [4, 5]
+    # seeded by the second-fastest pair: it leads, the fastest disjoint one follows
+    c2 = P.candidate_assignments(times, 8, names, 2)[2]
+    assert c2["theta"] == [2, 0] and c2["mom"] == [3, 1]
+
+
+def test_no_pair_times_gives_allocation_order_only():
+    names = ["theta", "grad", "mom"]
+    assert P.candidate_assignments({}, 6, names, 2) == [
+        {"theta": [0, 1], "grad": [2, 3], "mom": [4, 5]}]
