@@ -250,55 +250,63 @@ __device__ __forceinline__ void moments_elem(const MArgs& a, float x, float& p, 
   }
 }
 
-// Grid-stride sweep, U float4 groups per lane in flight: a block iteration
-// wholly inside the vector issues all its loads before any arithmetic, with no
-// bounds checks; only the last partial iteration takes the guarded path.
+template <int COLLECT, bool RECIP>
+__device__ __forceinline__ void moments4(const MArgs& a, const f4v t, f4v& m1, f4v& m2) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float p = m1[j], q = m2[j];
+    moments_elem<COLLECT, RECIP>(a, t[j], p, q);
+    m1[j] = p;
+    m2[j] = q;
+  }
+}
+
+// Grid-stride sweep, U float4 groups per lane in flight: an unguarded loop over
+// the block iterations wholly inside the vector (all loads issued before any
+// arithmetic), then at most one guarded iteration per block for the tail —
+// the loop shape of bdl_sample_kernel.
 template <int COLLECT, bool RECIP, bool M2, int U>
 __global__ __launch_bounds__(kBlock) void bdl_moments_kernel(const MArgs a) {
   constexpr bool kRead = COLLECT == BDL_COLLECT_WELFORD || COLLECT == BDL_COLLECT_MEAN;
   constexpr int64_t kIter = (int64_t)kBlock * U;
   const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * kIter;
   const f4v z = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {
-    const bool fast = gb + kIter <= nfull;
+  int64_t gb = (int64_t)blockIdx.x * kIter;
+  for (; gb + kIter <= nfull; gb += stride) {
     f4v t[U], m1[U], m2[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
-      const int64_t e = gi * 4;
-      m1[u] = m2[u] = t[u] = z;
-      if (fast) {
-        t[u] = vload(a.theta + e);
-        if constexpr (kRead) {
-          m1[u] = vload(a.mom1 + e);
-          if constexpr (M2) m2[u] = vload(a.mom2 + e);
-        }
-      } else if (gi < ngroups) {
-        t[u] = ld4(a.theta, e, a.n);
-        if constexpr (kRead) {
-          m1[u] = ld4(a.mom1, e, a.n);
-          if constexpr (M2) m2[u] = ld4(a.mom2, e, a.n);
-        }
+      const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+      m1[u] = m2[u] = z;
+      t[u] = vload(a.theta + e);
+      if constexpr (kRead) {
+        m1[u] = vload(a.mom1 + e);
+        if constexpr (M2) m2[u] = vload(a.mom2 + e);
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+      moments4<COLLECT, RECIP>(a, t[u], m1[u], m2[u]);
+      vstore(a.mom1 + e, m1[u]);
+      if constexpr (M2) vstore(a.mom2 + e, m2[u]);
+    }
+  }
+  if (gb < ngroups) {
+    for (int u = 0; u < U; ++u) {
       const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+      if (gi >= ngroups) break;
       const int64_t e = gi * 4;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float p = m1[u][j], q = m2[u][j];
-        moments_elem<COLLECT, RECIP>(a, t[u][j], p, q);
-        m1[u][j] = p;
-        m2[u][j] = q;
+      f4v m1 = z, m2 = z;
+      const f4v t = ld4(a.theta, e, a.n);
+      if constexpr (kRead) {
+        m1 = ld4(a.mom1, e, a.n);
+        if constexpr (M2) m2 = ld4(a.mom2, e, a.n);
       }
-      if (fast) {
-        vstore(a.mom1 + e, m1[u]);
-        if constexpr (M2) vstore(a.mom2 + e, m2[u]);
-      } else if (gi < ngroups) {
-        st4(a.mom1, e, a.n, m1[u]);
-        if constexpr (M2) st4(a.mom2, e, a.n, m2[u]);
-      }
+      moments4<COLLECT, RECIP>(a, t, m1, m2);
+      st4(a.mom1, e, a.n, m1);
+      if constexpr (M2) st4(a.mom2, e, a.n, m2);
     }
   }
 }
@@ -364,76 +372,96 @@ __device__ __forceinline__ float sample_var(const SArgs& a, float mj, float qj) 
   return var;
 }
 
-template <int VAR, bool M2, bool RECIP, int NOISE, int U>
+// FLOORED: the host saw var_floor >= 2^-96, so every variance is NaN or at
+// least 2^-96 and sqrt_floored gives sqrtf's bits with ~6 VALU ops fewer.
+template <int VAR, bool M2, bool RECIP, bool FLOORED>
+__device__ __forceinline__ f4v sample4(const SArgs& a, const f4v m, const f4v q, const f4v ep) {
+  f4v o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float var = sample_var<VAR, M2, RECIP>(a, m[j], q[j]);
+    o[j] = m[j] + (FLOORED ? sqrt_floored(var) : sqrtf(var)) * ep[j];
+  }
+  return o;
+}
+
+// Unguarded loop over the full block iterations (all loads first, then the
+// generator and the math, then the stores), then at most one guarded
+// iteration per block for the vector's tail.  Split this way the fast loop
+// carries no per-group range branch: 0.586-0.598 ms vs 0.608 ms for the
+// per-group-guarded loop at ViT-L/32 size (tools/sample_probe.hip,
+// profiles/round2/aux/sample_probe.jsonl).
+template <int VAR, bool M2, bool RECIP, int NOISE, bool FLOORED, int U>
 __global__ __launch_bounds__(kBlock) void bdl_sample_kernel(const SArgs a) {
   constexpr int64_t kIter = (int64_t)kBlock * U;
   const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * kIter;
   const f4v z = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {
-    const bool fast = gb + kIter <= nfull;
+  int64_t gb = (int64_t)blockIdx.x * kIter;
+  for (; gb + kIter <= nfull; gb += stride) {
     f4v m[U], q[U], ep[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
-      const int64_t e = gi * 4;
-      m[u] = q[u] = ep[u] = z;
-      if (fast) {
-        m[u] = vload(a.mom1 + e);
-        if constexpr (M2) q[u] = vload(a.mom2 + e);
-        if constexpr (NOISE == BDL_NOISE_BUFFER) ep[u] = vload(a.noise + e);
-      } else if (gi < ngroups) {
-        m[u] = ld4(a.mom1, e, a.n);
-        if constexpr (M2) q[u] = ld4(a.mom2, e, a.n);
-        if constexpr (NOISE == BDL_NOISE_BUFFER) ep[u] = ld4(a.noise, e, a.n);
-      }
+      const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+      m[u] = vload(a.mom1 + e);
+      q[u] = z;
+      if constexpr (M2) q[u] = vload(a.mom2 + e);
+      if constexpr (NOISE == BDL_NOISE_BUFFER) ep[u] = vload(a.noise + e);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+      if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = sample_noise4(a, gi);
+      vstore(a.out + gi * 4, sample4<VAR, M2, RECIP, FLOORED>(a, m[u], q[u], ep[u]));
+    }
+  }
+  if (gb < ngroups) {
+    for (int u = 0; u < U; ++u) {
+      const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+      if (gi >= ngroups) break;
       const int64_t e = gi * 4;
-      if constexpr (NOISE == BDL_NOISE_PHILOX)
-        ep[u] = sample_noise4(a, gi);
-      f4v o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        o[j] = m[u][j] + sqrtf(sample_var<VAR, M2, RECIP>(a, m[u][j], q[u][j])) * ep[u][j];
-      if (fast)
-        vstore(a.out + e, o);
-      else if (gi < ngroups)
-        st4(a.out, e, a.n, o);
+      const f4v m = ld4(a.mom1, e, a.n);
+      const f4v q = M2 ? ld4(a.mom2, e, a.n) : z;
+      const f4v ep = NOISE == BDL_NOISE_BUFFER ? ld4(a.noise, e, a.n) : sample_noise4(a, gi);
+      st4(a.out, e, a.n, sample4<VAR, M2, RECIP, FLOORED>(a, m, q, ep));
     }
   }
 }
 
 typedef void (*SampleKernel)(const SArgs);
 
-// Posterior-sample geometry: Philox makes this sweep VALU-heavy per byte (12 B
-// per element against ~65 VALU slots), so it runs at its own occupancy —
-// 3 workgroups per CU, 4 float4 groups per lane in flight (tools/aux_sweep.py,
-// profiles/round1/aux_sweep.log) — independent of the step kernels' tuning.
+// Posterior-sample geometry, independent of the step kernels' tuning: 2
+// workgroups per CU, 4 float4 groups per lane in flight — the best or within
+// 1 % of it on two boxes among {1,2,4} groups x {2,3,4} workgroups/CU for the
+// split loop (tools/sample_probe.hip, profiles/round2/aux/sample_probe*.jsonl;
+// the per-group-guarded loop of round 1 was best at 3).
 #ifndef BDL_SAMPLE_U
 #define BDL_SAMPLE_U 4
 #endif
 #ifndef BDL_SAMPLE_BPC
-#define BDL_SAMPLE_BPC 3
+#define BDL_SAMPLE_BPC 2
 #endif
 
-template <int NOISE>
+template <int NOISE, bool FL>
 SampleKernel pick_sample_n(int var_mode, bool m2, bool recip) {
   constexpr int U = BDL_SAMPLE_U;
-  if (!m2) return bdl_sample_kernel<BDL_VAR_GIVEN, false, false, NOISE, U>;
+  if (!m2) return bdl_sample_kernel<BDL_VAR_GIVEN, false, false, NOISE, FL, U>;
   switch (var_mode) {
-    case BDL_VAR_RAW_MOMENTS: return bdl_sample_kernel<BDL_VAR_RAW_MOMENTS, true, false, NOISE, U>;
+    case BDL_VAR_RAW_MOMENTS: return bdl_sample_kernel<BDL_VAR_RAW_MOMENTS, true, false, NOISE, FL, U>;
     case BDL_VAR_WELFORD:
-      return recip ? bdl_sample_kernel<BDL_VAR_WELFORD, true, true, NOISE, U>
-                   : bdl_sample_kernel<BDL_VAR_WELFORD, true, false, NOISE, U>;
-    default: return bdl_sample_kernel<BDL_VAR_GIVEN, true, false, NOISE, U>;
+      return recip ? bdl_sample_kernel<BDL_VAR_WELFORD, true, true, NOISE, FL, U>
+                   : bdl_sample_kernel<BDL_VAR_WELFORD, true, false, NOISE, FL, U>;
+    default: return bdl_sample_kernel<BDL_VAR_GIVEN, true, false, NOISE, FL, U>;
   }
 }
 
-SampleKernel pick_sample(int var_mode, bool m2, bool recip, int noise_mode) {
-  return noise_mode == BDL_NOISE_BUFFER ? pick_sample_n<BDL_NOISE_BUFFER>(var_mode, m2, recip)
-                                        : pick_sample_n<BDL_NOISE_PHILOX>(var_mode, m2, recip);
+// floored: var_floor >= 2^-96 (the Runners' 1e-12 clamp), see sqrt_floored
+SampleKernel pick_sample(int var_mode, bool m2, bool recip, int noise_mode, bool floored) {
+  if (noise_mode == BDL_NOISE_BUFFER)
+    return floored ? pick_sample_n<BDL_NOISE_BUFFER, true>(var_mode, m2, recip)
+                   : pick_sample_n<BDL_NOISE_BUFFER, false>(var_mode, m2, recip);
+  return floored ? pick_sample_n<BDL_NOISE_PHILOX, true>(var_mode, m2, recip)
+                 : pick_sample_n<BDL_NOISE_PHILOX, false>(var_mode, m2, recip);
 }
 
 __global__ __launch_bounds__(kBlock) void bdl_philox_kernel(float* __restrict__ out, int64_t n,
@@ -878,8 +906,9 @@ int bdl_posterior_sample(const bdl_sample_args* s, void* stream) {
   SArgs a{s->out, s->mom1, s->mom2, s->noise, s->n, s->var_mode, s->noise_mode,
           s->ratio, s->var_floor, s->inv_ratio, s->seed, s->chain, s->step,
           (uint32_t)s->chain_groups};
+  const bool floored = s->var_floor >= 0x1p-96f;  // false for NaN
   hipLaunchKernelGGL(pick_sample(s->var_mode, s->mom2 != nullptr, s->inv_ratio != 0.0f,
-                                 s->noise_mode),
+                                 s->noise_mode, floored),
                      dim3(grid_sample((s->n + 3) / 4)), dim3(kBlock), 0,
                      (hipStream_t)stream, a);
   const hipError_t err = hipGetLastError();

@@ -34,9 +34,29 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
   return c;
 }
 
-// uniform in (0, 1): 24 random bits, centred in their bucket -> never 0 or 1.
+// uniform in (0, 1]: 24 random bits, centred in their bucket; the value is
+// fl32((x>>8) + 0.5) * 2^-24 (the top bucket rounds to 1.0).  Written as one
+// fma: scaling by a power of two commutes with the rounding, so
+// fma(a, 2^-24, 2^-25) == (a + 0.5f) * 2^-24 bit for bit for every 24-bit a
+// (checked over all 2^24 inputs, tools/sample_probe.hip) — one VALU op fewer
+// per draw.
 __device__ __forceinline__ float u01(uint32_t x) {
-  return ((float)(x >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  return __builtin_fmaf((float)(x >> 8), 1.0f / 16777216.0f, 1.0f / 33554432.0f);
+}
+
+// Correctly rounded fp32 sqrt for x >= 2^-96, +inf and NaN (bit-identical to
+// sqrtf there; checked over every such float, tools/sample_probe.hip):
+// v_sqrt_f32 (within 1 ulp) and the two-sided fma residual correction of the
+// compiler's own sequence, without its denormal-range scaling and its
+// zero / inf class fix-up, which that domain never needs.
+__device__ __forceinline__ float sqrt_floored(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float dn = __int_as_float(__float_as_int(s) - 1);
+  const float up = __int_as_float(__float_as_int(s) + 1);
+  const float rdn = __builtin_fmaf(-dn, s, x);
+  const float rup = __builtin_fmaf(-up, s, x);
+  const float r = rdn <= 0.f ? dn : s;
+  return rup > 0.f ? up : r;
 }
 
 // Four N(0,1) draws for flat elements 4*group .. 4*group+3.

@@ -1,0 +1,100 @@
+"""Config 5 rehearsed on one MI355X: ViT-L/32 cSGHMC, 8 independent chains
+(8 processes, one chain each, sharing the box's GPU over gloo — the same
+bayesdll_amd.chains calls RCCL makes with one GPU per rank), each trained with
+the product Runner at full model size (306,535,400 parameters), then the
+cross-chain posterior-predictive average.
+
+Checks:
+  * every rank samples its own chain (chain id = rank; eight distinct thetas);
+  * chain 7 of the ensemble is, bit for bit, the chain one process samples
+    alone with chain id 7 (no cross-chain coupling during sampling);
+  * every rank's predictive is log((1/8) sum_k softmax(s_k)) of the chains' own
+    mixture predictives, rebuilt here from each rank's per-chain posterior
+    draws (logits_all), and all ranks hold the same one.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+pytestmark = pytest.mark.gpu
+WORLD = 8  # config 5's chain count
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.timeout(900)
+def test_config5_eight_vit_chains_one_gpu(tmp_path):
+    port = _free_port()
+    procs, outs = [], []
+    # chunks in allocation order: eight concurrent placement searches on one GPU
+    # would time each other, and their transient candidate sets add up
+    env0 = dict(os.environ, BDL_PLACEMENT="order")
+    for r in range(WORLD):
+        out = str(tmp_path / f"rank{r}.npz")
+        env = dict(env0, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(WORLD),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "config5_worker.py"),
+                                       "--out", out], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+        outs.append(out)
+    logs = []
+    try:
+        for p in procs:
+            logs.append(p.communicate(timeout=780)[0].decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-3000:]
+    ranks = [dict(np.load(o)) for o in outs]
+
+    assert all(int(r["n"]) == 306535400 for r in ranks)
+    for k, r in enumerate(ranks):
+        assert int(r["chain"]) == k
+        assert np.isfinite(r["theta_sum"]) and np.isfinite(r["loss"])
+    assert len({int(r["theta_bits"]) for r in ranks}) == WORLD  # eight distinct chains
+
+    os.environ["BDL_PLACEMENT"] = "order"
+    try:
+        from config5_worker import run_chain
+        single = run_chain(chain=WORLD - 1)
+    finally:
+        os.environ.pop("BDL_PLACEMENT", None)
+    last = ranks[WORLD - 1]
+    assert int(single["theta_bits"]) == int(last["theta_bits"])
+    assert single["theta_sum"] == last["theta_sum"]
+    np.testing.assert_array_equal(single["theta_sub"], last["theta_sub"])
+    np.testing.assert_array_equal(single["logits_all"], last["logits_all"])
+
+    # each chain's own mixture predictive from its draws: one cycle, nst draws
+    def chain_pred(r):
+        comp = torch.from_numpy(r["logits_all"]).double()  # [B, C, nst, cycles]
+        w = torch.from_numpy(r["weights"])
+        lp = torch.log_softmax(comp, 1).logsumexp(2) - np.log(comp.shape[2])
+        return (lp * w).sum(-1)
+    preds = torch.stack([torch.log_softmax(chain_pred(r), 1) for r in ranks])
+    want = (torch.logsumexp(preds, 0) - np.log(WORLD)).numpy()
+    for r in ranks:
+        np.testing.assert_array_equal(r["targets"], ranks[0]["targets"])
+        np.testing.assert_allclose(r["logits"], want, rtol=0, atol=5e-6)
+        np.testing.assert_array_equal(r["logits"], ranks[0]["logits"])
