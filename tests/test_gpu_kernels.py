@@ -285,6 +285,42 @@ def test_posterior_sample_matches_torch_formula():
     assert torch.equal(out, m1 + torch.full_like(m1, 1e-12).sqrt() * eps)
 
 
+@pytest.mark.parametrize("floor", [1e-12, 2.0 ** -96, 2.0 ** -97, 1e-40, 0.0])
+def test_posterior_sample_sqrt_at_every_floor(floor):
+    """The sample sweep takes v_sqrt_f32 + residual correction when the floor
+    is >= 2^-96 and the compiler's full sqrtf otherwise: both give torch's
+    device sqrt bit for bit over variances spanning zero, subnormals, the
+    2^-96 boundary, large values and inf (NaN stays NaN)."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    g = torch.Generator(device=DEV).manual_seed(5)
+    n = (1 << 20) + 7  # a partial last iteration and a partial last float4 group
+    e = torch.randint(-149, 128, (n,), device=DEV, generator=g).float()
+    var = torch.rand(n, device=DEV, generator=g) * torch.exp2(e)  # every binade, subnormals too
+    var[:64] = torch.tensor([0.0, 2.0 ** -96, 2.0 ** -97, 2.0 ** -95, 1e-45, float("inf"),
+                             float("nan"), 3.4e38] * 8, device=DEV)
+    m1 = torch.randn(n, device=DEV, generator=g)
+    eps = torch.randn(n, device=DEV, generator=g)
+    out = torch.empty_like(m1)
+    K.posterior_sample(out, m1, var, var_mode=L.VAR_GIVEN, var_floor=floor, noise=eps)
+    v = var.clone()
+    keep = torch.isnan(v)
+    v = torch.where(keep, v, v.clamp(min=torch.tensor(floor, dtype=torch.float32).item()))
+    want = m1 + v.sqrt() * eps
+    torch.cuda.synchronize()
+    nan = torch.isnan(want)
+    assert torch.equal(torch.isnan(out), nan)
+    assert torch.equal(out[~nan].view(torch.int32), want[~nan].view(torch.int32))
+    # and with Philox noise: the stream the buffer mode is fed by bdl_philox_normal
+    K.posterior_sample(out, m1, var, var_mode=L.VAR_GIVEN, var_floor=floor, seed=9, chain=2, step=4)
+    z = K.philox_normal(n, 9, 2, 4, device=DEV)
+    want = m1 + v.sqrt() * z
+    torch.cuda.synchronize()
+    nan = torch.isnan(want)
+    assert torch.equal(torch.isnan(out), nan)
+    assert torch.equal(out[~nan].view(torch.int32), want[~nan].view(torch.int32))
+
+
 # ------------------------------------------------------- clipped SGLD (csgld)
 def ref_clip_sgld(st, max_norm, lrs, ns, sigma, N, mu, first):
     """methods/csgld.py:250-253 on the device with torch ops: the sampler
