@@ -402,12 +402,22 @@ __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, i
   constexpr bool kPriorLoad = T::kReadPrior && PRIOR && !GR;
   f4v th[UNROLL], g[UNROLL], v[UNROLL], t0[UNROLL], ep[UNROLL], m1[UNROLL], m2[UNROLL];
   const f4v z = {0.f, 0.f, 0.f, 0.f};
+#ifdef BDL_LOAD_STREAM_MAJOR
+  // A/B experiment (tools/step_ab.py): theta, grad, mom each issued for all
+  // unrolled groups before the next stream, instead of group by group
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) th[u] = vload(a.theta + (gb + (int64_t)u * kBlock + threadIdx.x) * 4);
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) g[u] = vload(gp + (gb + (int64_t)u * kBlock + threadIdx.x) * 4);
+#endif
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
     const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
     v[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
+#ifndef BDL_LOAD_STREAM_MAJOR
     th[u] = vload(a.theta + e);
     g[u] = vload(gp + e);
+#endif
     if constexpr (T::kMom) v[u] = vload(a.mom + e);
     if constexpr (METHOD == BDL_SGLD) {
       if (c.sgd_mom_read) v[u] = vload(a.mom + e);

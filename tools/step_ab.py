@@ -1,0 +1,91 @@
+"""Same-process A/B of library builds on the fused ViT-L/32 cSGHMC step
+(tooling).  One FlatState (physical-chunk placement, theta / mom on the fast
+pairing), then for every build in argv and every launch geometry, the explore
+step (theta rw, grad r, mom rw) and the Welford collect step, HIP-event mean
+over 20 launches, builds alternating A, B, C, ... for ROUNDS rounds — so a
+build's number is never a different placement's number.
+
+  python tools/step_ab.py LIB [LIB ...]     (ROUNDS=4, GEOMS="1,4,1;2,1,1;1,2,1;1,4,0")
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bayesdll_amd import _lib as L  # noqa: E402
+from bayesdll_amd import kernels as K  # noqa: E402
+from bayesdll_amd.flat import FlatState  # noqa: E402
+from bayesdll_amd.shapes import segments  # noqa: E402
+
+libs = [os.path.abspath(p) for p in sys.argv[1:]]
+rounds = int(os.environ.get("ROUNDS", "4"))
+geoms = [tuple(int(x) for x in g.split(",")) for g in
+         os.environ.get("GEOMS", "1,4,1;2,1,1;1,2,1;1,4,0").split(";")]
+dev = torch.device("cuda", 0)
+
+
+def use(path):
+    L._lib = None
+    L.LIB_PATH = path
+    L.lib()
+
+
+use(libs[0])
+segs, readout = segments("vit_l_32", 1000)
+st = FlatState.from_segments(segs, readout, device=dev, placement="csghmc")
+gen = torch.Generator(device=dev).manual_seed(1)
+st.theta.normal_(0.0, 0.02, generator=gen)
+st.grad.normal_(0.0, 1e-3, generator=gen)
+m1 = st.theta.clone()
+m2 = torch.zeros_like(st.theta)
+n = st.n
+print(json.dumps({"placement": {k: st.placement_info.get(k) for k in
+                                ("allocator", "chosen_ms", "untuned_torch_ms", "kept")}}),
+      flush=True)
+lrs, alpha, N = (1e-4, 1e-2), 0.18, 1840.0
+
+
+def explore(i):
+    K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=(0.0, 0.0), noise_mode=L.NOISE_NONE,
+                  one_minus_alpha=1 - alpha, prior_sig=1.0)
+
+
+def collect(i):
+    ns = [0.01 * np.sqrt(2 * alpha * x) / N for x in lrs]
+    K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_PHILOX,
+                  one_minus_alpha=1 - alpha, prior_sig=1.0, collect=L.COLLECT_WELFORD, mom1=m1,
+                  mom2=m2, collect_a=float(i + 3), seed=3, chain=0, step=i)
+
+
+def t(fn, reps=20):
+    for i in range(3):
+        fn(i)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(reps):
+        fn(i)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+res = {}
+for r in range(rounds):
+    for path in libs:
+        use(path)
+        for g in geoms:
+            K.set_launch_config(*g)
+            for name, fn, bpe in (("explore", explore, 20), ("collect", collect, 36)):
+                if name == "collect" and g != geoms[0]:
+                    continue
+                ms = t(fn)
+                res.setdefault((os.path.basename(path), g, name), []).append(ms)
+                print(json.dumps({"round": r, "lib": os.path.basename(path), "geom": g,
+                                  "kernel": name, "ms": round(ms, 4),
+                                  "frac": round(bpe * n / ms / 1e6 / 8000.0, 4)}), flush=True)
+for (lib, g, name), v in sorted(res.items(), key=lambda kv: (kv[0][2], np.median(kv[1]))):
+    print(json.dumps({"summary": name, "lib": lib, "geom": g, "median_ms": round(float(np.median(v)), 4),
+                      "min_ms": round(min(v), 4)}))
