@@ -508,6 +508,12 @@ StepKernel pick_probe(int method, int noise, int collect) {
   return nullptr;
 }
 
+// A/B flavours only (make flavor D=-DBDL_GRID_PCT=75): the step grid as a
+// percentage of workgroups/CU x CUs
+#ifndef BDL_GRID_PCT
+#define BDL_GRID_PCT 100
+#endif
+
 int grid_for(int64_t ngroups, int per_block_groups) {
   const int64_t want = (ngroups + per_block_groups - 1) / per_block_groups;
   const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
@@ -588,7 +594,7 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
 
   const int64_t ngroups = (s->n + 3) / 4;
   const int64_t per_iter = (int64_t)kBlock * unroll;
-  const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
+  const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu * BDL_GRID_PCT / 100;
   int64_t iters = (ngroups + per_iter - 1) / per_iter;
   int64_t grid = std::max<int64_t>(1, std::min(iters, cap));
   int64_t iters_per_block = (iters + grid - 1) / grid;

@@ -860,6 +860,12 @@ __global__ __launch_bounds__(kBlock) void bdl_adam_kernel(const KArgs a) {
 // ---------------------------------------------------------------------------
 using StepKernel = void (*)(const KArgs);
 
+// A/B flavours only (make flavor D=-DBDL_DEEP_UNROLL=8): the depth that an
+// unroll-4 request runs at
+#ifndef BDL_DEEP_UNROLL
+#define BDL_DEEP_UNROLL 4
+#endif
+
 template <int METHOD, int NOISE, int COLLECT>
 StepKernel pick_unroll(int unroll) {
   // Every unroll depth for cSGHMC and for the noise-bearing SGHMC / SGLD
@@ -876,7 +882,7 @@ StepKernel pick_unroll(int unroll) {
       case 1:
         return bdl_step_kernel<METHOD, NOISE, COLLECT, 1>;
       case 4:
-        return bdl_step_kernel<METHOD, NOISE, COLLECT, 4>;
+        return bdl_step_kernel<METHOD, NOISE, COLLECT, BDL_DEEP_UNROLL>;
       default:
         return bdl_step_kernel<METHOD, NOISE, COLLECT, 2>;
     }
