@@ -9,8 +9,8 @@ random-init ViT-L/32 (306,535,400 parameters, 296 tensors) and synthetic
 224 x 224 batches.  Run as a script under a torch.distributed environment
 every process is one chain (chain id = rank) and Runner.evaluate averages the
 predictive across the chains with bayesdll_amd.chains; the ranks share the
-box's one GPU over gloo (RCCL needs one GPU per rank).  The full theta does not
-travel: the worker returns exact checksums of it (float64 sum, the int64 sum of
+box's one GPU over gloo (RCCL needs one GPU per rank); with --chain K the
+process samples chain K alone.  The full theta does not travel: the worker returns exact checksums of it (float64 sum, the int64 sum of
 its bit patterns) and a strided subsample.
 """
 from __future__ import annotations
@@ -50,7 +50,35 @@ def theta_digest(theta):
             theta[::4099].detach().cpu().numpy())
 
 
+class deterministic_autograd:
+    """The reference demos' determinism (demo_mnist.py:74 sets
+    cudnn.deterministic) plus the math attention backend: MIOpen's default
+    convolution algorithms and the fused attention kernels' backward can
+    differ run to run, which would hide whether the SAMPLER couples chains.
+    Restores the previous settings on exit (the test process runs others)."""
+
+    def __enter__(self):
+        b = torch.backends
+        self.saved = (b.cudnn.deterministic, b.cudnn.benchmark, b.cuda.flash_sdp_enabled(),
+                      b.cuda.mem_efficient_sdp_enabled())
+        b.cudnn.deterministic, b.cudnn.benchmark = True, False
+        b.cuda.enable_flash_sdp(False)
+        b.cuda.enable_mem_efficient_sdp(False)
+        return self
+
+    def __exit__(self, *exc):
+        b = torch.backends
+        b.cudnn.deterministic, b.cudnn.benchmark = self.saved[0], self.saved[1]
+        b.cuda.enable_flash_sdp(self.saved[2])
+        b.cuda.enable_mem_efficient_sdp(self.saved[3])
+
+
 def run_chain(chain=None):
+    with deterministic_autograd():
+        return _run_chain(chain)
+
+
+def _run_chain(chain=None):
     import bayesdll_amd.csghmc as csghmc
     from bayesdll_amd.backbones import backbone
     dev = "cuda"
@@ -83,7 +111,12 @@ def run_chain(chain=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
+    ap.add_argument("--chain", type=int, default=None,
+                    help="one process alone with this chain id (no torch.distributed)")
     a = ap.parse_args()
+    if a.chain is not None:
+        np.savez(a.out, **run_chain(chain=a.chain))
+        return
     from bayesdll_amd import chains
     chains.init_chains(backend="gloo")
     try:

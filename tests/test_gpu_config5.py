@@ -40,25 +40,18 @@ def _free_port():
     return port
 
 
-@pytest.mark.timeout(900)
-def test_config5_eight_vit_chains_one_gpu(tmp_path):
-    port = _free_port()
+def _run(tmp_path, envs, extra, tag):
     procs, outs = [], []
-    # chunks in allocation order: eight concurrent placement searches on one GPU
-    # would time each other, and their transient candidate sets add up
-    env0 = dict(os.environ, BDL_PLACEMENT="order")
-    for r in range(WORLD):
-        out = str(tmp_path / f"rank{r}.npz")
-        env = dict(env0, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(WORLD),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    for i, (env, ex) in enumerate(zip(envs, extra)):
+        out = str(tmp_path / f"{tag}{i}.npz")
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "config5_worker.py"),
-                                       "--out", out], env=env,
+                                       "--out", out, *ex], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
         outs.append(out)
     logs = []
     try:
         for p in procs:
-            logs.append(p.communicate(timeout=780)[0].decode(errors="replace"))
+            logs.append(p.communicate(timeout=600)[0].decode(errors="replace"))
     finally:
         for p in procs:
             if p.poll() is None:
@@ -66,7 +59,24 @@ def test_config5_eight_vit_chains_one_gpu(tmp_path):
                 p.wait()
     for p, log in zip(procs, logs):
         assert p.returncode == 0, log[-3000:]
-    ranks = [dict(np.load(o)) for o in outs]
+    return [dict(np.load(o)) for o in outs]
+
+
+@pytest.mark.timeout(900)
+def test_config5_eight_vit_chains_one_gpu(tmp_path):
+    port = _free_port()
+    # chunks in allocation order: eight concurrent placement searches on one GPU
+    # would time each other, and their transient candidate sets add up
+    env0 = dict(os.environ, BDL_PLACEMENT="order")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env0.pop(k, None)
+    envs = [dict(env0, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(WORLD),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port)) for r in range(WORLD)]
+    ranks = _run(tmp_path, envs, [[] for _ in range(WORLD)], "rank")
+    # the chain one process samples alone with chain id 7, in a fresh process
+    # like the ranks (a process that has already run other GPU work can get
+    # other autograd kernels from the libraries, tools/vit_concurrent.py)
+    single = _run(tmp_path, [env0], [["--chain", str(WORLD - 1)]], "single")[0]
 
     assert all(int(r["n"]) == 306535400 for r in ranks)
     for k, r in enumerate(ranks):
@@ -74,12 +84,6 @@ def test_config5_eight_vit_chains_one_gpu(tmp_path):
         assert np.isfinite(r["theta_sum"]) and np.isfinite(r["loss"])
     assert len({int(r["theta_bits"]) for r in ranks}) == WORLD  # eight distinct chains
 
-    os.environ["BDL_PLACEMENT"] = "order"
-    try:
-        from config5_worker import run_chain
-        single = run_chain(chain=WORLD - 1)
-    finally:
-        os.environ.pop("BDL_PLACEMENT", None)
     last = ranks[WORLD - 1]
     assert int(single["theta_bits"]) == int(last["theta_bits"])
     assert single["theta_sum"] == last["theta_sum"]
