@@ -102,7 +102,12 @@ def main():
     ap.add_argument("--method", required=True, choices=sorted(HPARAMS))
     ap.add_argument("--out", required=True)
     ap.add_argument("--replica", action="store_true")
+    ap.add_argument("--chain", type=int, default=None,
+                    help="one process alone with this chain id (no torch.distributed)")
     a = ap.parse_args()
+    if a.chain is not None:
+        np.savez(a.out, **run_chain(a.method, chain=a.chain))
+        return
     from bayesdll_amd import chains
     chains.init_chains(backend="gloo")  # ranks share one GPU here; RCCL needs one GPU per rank
     try:

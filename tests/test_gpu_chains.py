@@ -39,15 +39,22 @@ def _free_port():
     return port
 
 
-def _run_ranks(method, tmp_path, extra=()):
+def _run_ranks(method, tmp_path, extra=(), singles=False):
+    """WORLD ranks of one ensemble, or (singles=True) WORLD single-chain
+    processes with chain ids 0..WORLD-1 and no torch.distributed — fresh
+    processes either way, so both sides start from the same library state."""
     port = _free_port()
     procs, outs = [], []
+    base = {k: v for k, v in os.environ.items()
+            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
     for r in range(WORLD):
-        out = str(tmp_path / f"{method}_rank{r}.npz")
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(WORLD),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        tag = "single" if singles else "rank"
+        out = str(tmp_path / f"{method}_{tag}{r}.npz")
+        env = base if singles else dict(base, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(WORLD),
+                                        MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        args = ["--chain", str(r)] if singles else list(extra)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "chain_worker.py"),
-                                       "--method", method, "--out", out, *extra], env=env,
+                                       "--method", method, "--out", out, *args], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
         outs.append(out)
     logs = []
@@ -66,9 +73,8 @@ def _run_ranks(method, tmp_path, extra=()):
 
 @pytest.mark.parametrize("method", ["csghmc", "sgld"])
 def test_two_chain_ensemble_matches_single_chains(method, tmp_path):
-    from chain_worker import run_chain
     ranks = _run_ranks(method, tmp_path)
-    singles = [run_chain(method, chain=r) for r in range(WORLD)]
+    singles = _run_ranks(method, tmp_path, singles=True)
     for r in range(WORLD):
         assert int(ranks[r]["chain"]) == r
         # each chain writes its checkpoints / logits under <log_dir>/chain<rank>
@@ -96,9 +102,8 @@ def test_sharded_likelihood_pass_and_gmm_weights_over_chains(tmp_path):
     loss sums) equals the single-process pass (rtol 1e-6); ranks whose
     moments differ are refused; evaluate() with GMM weights over chains gives
     the single chain's predictive when the chains are identical."""
-    from chain_worker import run_chain
     ranks = _run_ranks("csghmc", tmp_path, extra=("--replica",))
-    single = run_chain("csghmc", chain=0)
+    single = _run_ranks("csghmc", tmp_path, singles=True)[0]
     for r in range(WORLD):
         np.testing.assert_array_equal(ranks[r]["theta"], single["theta"])
         np.testing.assert_array_equal(ranks[r]["lik_local"], single["lik_local"])
