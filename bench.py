@@ -566,6 +566,16 @@ def main():
                                         if traffic is not None else None),
                      "alg_bytes_per_launch": alg_bytes},
     }
+    if dist is not None:
+        # every rank's own dominant-kernel time and placement (rank 0's is the
+        # roofline above): the slowest GPU sets the aggregate's wall clock
+        mine = {"rank": rank, "kernel": dominant, "avg_ms": dom["avg_ms"],
+                "placement_ms": (st.placement_info or {}).get("chosen_ms")}
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+        out["per_rank"] = [{"rank": r["rank"], "kernel": r["kernel"], "avg_ms": r["avg_ms"],
+                            "frac": round(alg_bytes / (r["avg_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                            "placement_ms": r["placement_ms"]} for r in allr]
     if not a.no_aux:
         out["aux_kernels"] = aux_kernels(st)
         try:  # HBM bytes per launch of the same sweeps from the committed PMC profile

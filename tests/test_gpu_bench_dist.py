@@ -61,12 +61,17 @@ def test_bench_two_ranks_gloo(launcher):
     assert ec["backend"] == "gloo" and ec["finite"] is True
     assert "cpu_baseline" not in d  # rank 0 at N=1 only
     assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
+    pr = d["per_rank"]  # every rank's own dominant-kernel time
+    assert [r["rank"] for r in pr] == [0, 1]
+    assert all(r["kernel"] == d["roofline"]["kernel"] and r["avg_ms"] > 0 and 0 < r["frac"] < 1
+               for r in pr)
 
 
 def test_rccl_process_group_init_as_bench_does():
     """The RCCL ("nccl") process-group calls bench.py's N-GPU path makes —
     init_process_group with device_id, barrier, all_reduce(MAX) of the timing,
-    the chains collectives on device tensors — in a one-rank group on the box's
+    the chains collectives on device tensors, all_gather_object of the
+    per-rank kernel times — in a one-rank group on the box's
     GPU (several ranks need one GPU each)."""
     code = r'''
 import os, torch, torch.distributed as dist
@@ -80,6 +85,9 @@ x = torch.ones(1 << 20, device="cuda")
 dist.all_reduce(x)
 lp = torch.log_softmax(torch.randn(8, 10, device="cuda"), 1)
 assert torch.equal(chains.average_predictive(lp), lp)
+got = [None]
+dist.all_gather_object(got, {"rank": 0, "avg_ms": 1.0})
+assert got == [{"rank": 0, "avg_ms": 1.0}]
 torch.cuda.synchronize()
 print("RCCL_OK", dist.get_backend(), float(t.item()), float(x[0].item()))
 dist.destroy_process_group()
