@@ -9,7 +9,6 @@ import itertools
 import json
 import sys
 
-import numpy as np
 import torch
 
 sys.path.insert(0, ".")
