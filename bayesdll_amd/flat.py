@@ -110,6 +110,9 @@ def _time_launch(launch, device, reps=5):
     return float(np.median([a.elapsed_time(b) for a, b in ev]))
 
 
+PLACEMENT_BPC = {"csghmc": 1, "sgld": 2, "adam": 2}
+
+
 def placed_vectors(n, device, names, method):
     """Allocate the chain's swept fp32 vectors (`names` among theta, grad, mom,
     prior, extra state), zeroed.  With `method` (the sampler's kernel family)
@@ -137,9 +140,12 @@ def placed_vectors(n, device, names, method):
         return _placement_launcher(method, roles, m, device, runs_by_n[m])
 
     from . import kernels as K
-    # one workgroup per CU for every placement timing (the probe kernel's depth
-    # is fixed at 4), whatever geometry another state installed
-    prev = K.set_launch_config(1, 4, 1)
+    # the probe kernel's depth is fixed at 4; workgroups per CU: the method's
+    # usual optimum at that depth (cSGHMC 1, the VALU-heavier SGLD / Adam
+    # sweeps 2 — at 1 they are occupancy-bound and placement barely shows),
+    # whatever geometry another state installed; BDL_PLACEMENT_BPC overrides
+    bpc = int(os.environ.get("BDL_PLACEMENT_BPC", "0")) or PLACEMENT_BPC.get(method, 1)
+    prev = K.set_launch_config(bpc, 4, 1)
     try:
         vecs, info = P.place(n, device, names, launcher, lambda f: _time_launch(f, device, 5),
                              budget_bytes=int(0.25 * free), search=mode == "search")
