@@ -559,14 +559,18 @@ def runs_ptr(state):
     return C.c_void_p(state.runs.data_ptr())
 
 
-def bind_parameters(net):
-    """Rebind `net`'s parameters as views of ONE new flat fp32 buffer (values
-    copied) and drop their grads; returns the buffer.  Used for the evaluation
-    copies whose theta the posterior-sample kernel writes in one sweep."""
+def bind_parameters(net, flat=None):
+    """Rebind `net`'s parameters as views of ONE flat fp32 buffer (a new one,
+    or `flat`; values copied) and drop their grads; returns the buffer.  Used
+    for the evaluation copies whose theta the posterior-sample kernel writes
+    in one sweep."""
     params = list(net.parameters())
     n = sum(p.numel() for p in params)
     dev = params[0].device
-    flat = torch.empty(n, dtype=torch.float32, device=dev)
+    if flat is None:
+        flat = torch.empty(n, dtype=torch.float32, device=dev)
+    elif flat.numel() != n or flat.dtype != torch.float32 or flat.device != dev:
+        raise ValueError("bind_parameters: flat buffer does not match the network")
     off = 0
     with torch.no_grad():
         for p in params:
@@ -576,6 +580,26 @@ def bind_parameters(net):
             p.grad = None
             off += k
     return flat
+
+
+DRAW_CANDIDATES = 3  # output buffers timed for the posterior-draw sweep
+
+
+def draw_buffer(out, launch, candidates=DRAW_CANDIDATES):
+    """Pick the posterior-draw output buffer (DESIGN.md §4 placement: the draw
+    reads m1 / m2 and writes out, and runs 3-4 % faster with out in the
+    physical class opposite to its reads, which only timing reveals).
+    `launch(buf)` runs the draw into `buf`; `out` and candidates - 1 fresh
+    allocations of its size are each timed (median of 3) and the fastest is
+    returned with the timings; the others go back to torch's cache.  Vectors
+    below PLACEMENT_MIN_ELEMS, or BDL_PLACEMENT=0: `out` unchanged."""
+    import os
+    if out.numel() < PLACEMENT_MIN_ELEMS or os.environ.get("BDL_PLACEMENT", "search") == "0":
+        return out, None
+    cands = [out] + [torch.empty_like(out) for _ in range(max(0, candidates - 1))]
+    ms = [_time_launch(lambda b=b: launch(b), out.device, 3) for b in cands]
+    best = int(np.argmin(ms))
+    return cands[best], [round(t, 4) for t in ms]
 
 
 def fill_normal_per_tensor(vec, numels, generator=None):

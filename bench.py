@@ -218,8 +218,14 @@ def aux_kernels(st, reps=20):
         res[name] = {"avg_ms": round(ms, 4), "bytes_per_elem": nbytes, "gbs": round(gbs, 1),
                      "frac": round(gbs / PEAK_HBM_GBS, 4)}
 
+    # the output buffer chosen as the Runners' posterior draws choose it
+    # (flat.draw_buffer: the plain allocation first, then fresh ones, timed)
+    from bayesdll_amd.flat import draw_buffer
+    out, cand_ms = draw_buffer(out, lambda b: K.posterior_sample(
+        b, m1, m2, var_mode=L.VAR_WELFORD, ratio=4.0, seed=7, chain=0, step=0))
     timed("posterior_sample", 12, lambda i: K.posterior_sample(
         out, m1, m2, var_mode=L.VAR_WELFORD, ratio=4.0, seed=7, chain=0, step=i))
+    res["posterior_sample"]["out_candidates_ms"] = cand_ms
     timed("moments_update", 20, lambda i: K.moments_update(
         st.theta, m1, m2, L.COLLECT_MEAN, collect_a=float(i + 1), collect_b=float(i + 2)))
     del m1, m2, out
