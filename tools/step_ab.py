@@ -33,9 +33,13 @@ def use(path):
     L.lib()
 
 
+METHOD = os.environ.get("METHOD", "csghmc")  # or "adam": the Adam-SGHMC + SGD step
 use(libs[0])
 segs, readout = segments("vit_l_32", 1000)
-st = FlatState.from_segments(segs, readout, device=dev, placement="csghmc")
+adam = METHOD == "adam"
+st = FlatState.from_segments(segs, readout, device=dev, placement="adam" if adam else "csghmc",
+                             need_prior=adam,
+                             extra=("adam_m", "adam_v", "sgd_buf") if adam else ())
 gen = torch.Generator(device=dev).manual_seed(1)
 st.theta.normal_(0.0, 0.02, generator=gen)
 st.grad.normal_(0.0, 1e-3, generator=gen)
@@ -49,6 +53,12 @@ lrs, alpha, N = (1e-4, 1e-2), 0.18, 1840.0
 
 
 def explore(i):
+    if adam:  # methods/adam_sghmc.py:458-553 + SGD(momentum 0.5), Philox
+        K.adam_step(st, L.ADAM_SGHMC, adam_m=st.extra["adam_m"], adam_v=st.extra["adam_v"],
+                    sgd_buf=st.extra["sgd_buf"], beta1=0.9, beta2=0.999, eps=1e-8, t=i + 2,
+                    momentum_decay=alpha, nd=0.01, lrs=lrs, noise_mode=L.NOISE_PHILOX,
+                    sigma2=1.0, n_data=N * 1e3, mu=0.5, momentum=True, seed=3, chain=0, step=i)
+        return
     K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=(0.0, 0.0), noise_mode=L.NOISE_NONE,
                   one_minus_alpha=1 - alpha, prior_sig=1.0)
 
@@ -78,8 +88,9 @@ for r in range(rounds):
         use(path)
         for g in geoms:
             K.set_launch_config(*g)
-            for name, fn, bpe in (("explore", explore, 20), ("collect", collect, 36)):
-                if name == "collect" and g != geoms[0]:
+            for name, fn, bpe in (("adam" if adam else "explore", explore, 48 if adam else 20),
+                                  ("collect", collect, 36)):
+                if name == "collect" and (g != geoms[0] or adam):
                     continue
                 ms = t(fn)
                 res.setdefault((os.path.basename(path), g, name), []).append(ms)
