@@ -64,3 +64,23 @@ def test_no_pair_times_gives_allocation_order_only():
     names = ["theta", "grad", "mom"]
     assert P.candidate_assignments({}, 6, names, 2) == [
         {"theta": [0, 1], "grad": [2, 3], "mom": [4, 5]}]
+
+
+def test_draw_buffer_keeps_small_vectors_and_honours_placement_off(monkeypatch):
+    """flat.draw_buffer times candidates only for vectors of >= PLACEMENT_MIN_ELEMS
+    with placement on; otherwise it returns the draw's own buffer untouched and
+    never launches."""
+    import torch
+
+    from bayesdll_amd import flat as F
+
+    def launch(_):
+        raise AssertionError("no launch expected")
+
+    small = torch.empty(F.PLACEMENT_MIN_ELEMS - 1)
+    assert F.draw_buffer(small, launch) == (small, None)
+    monkeypatch.setenv("BDL_PLACEMENT", "0")
+    big = torch.empty(F.PLACEMENT_MIN_ELEMS)
+    out, ms = F.draw_buffer(big, launch)
+    assert out is big and ms is None
+
