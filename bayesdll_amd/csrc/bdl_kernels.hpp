@@ -525,9 +525,20 @@ __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, i
     if (gi >= gend) continue;
     const int64_t e = gi * 4;
     const f4v z = {0.f, 0.f, 0.f, 0.f};
-    const bool gt = a.gbase != nullptr;  // gradient per tensor: element-wise below
+    const bool gt = a.gbase != nullptr;  // gradient per tensor
     f4v th = ld4(a.theta, e, n), g = gt ? z : ld4(a.grad, e, n), v = z, t0 = z, ep = z, m1 = z,
         m2 = z;
+    // per-tensor gradient: one 16-B load when the group lies in one run whose
+    // base is 16-B addressable (run offsets are multiples of 4 on every
+    // backbone here), else element by element below
+    bool gvec = false;
+    if (gt) {
+      while (rr < a.nruns - 1 && run_end(rr) <= e) ++rr;
+      if (e + 4 <= n && run_end(rr) >= e + 4 && !(run_attr(rr) & kNoFastPath)) {
+        g = vload(run_grad(a, rr) + e);
+        gvec = true;
+      }
+    }
     if (T::kMom || (METHOD == BDL_SGLD && c.sgd_mom_read)) v = ld4(a.mom, e, n);
     if (T::kReadPrior) t0 = ld4(a.prior_mean, e, n);
     if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, n);
@@ -542,7 +553,7 @@ __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, i
       while (rr < a.nruns - 1 && run_end(rr) <= e + j) ++rr;
       const uint32_t at = run_attr(rr);
       float* gpr = gt ? run_grad(a, rr) : nullptr;
-      if (gt && !(at & BDL_ATTR_SKIP)) g[j] = gpr[e + j];
+      if (gt && !gvec && !(at & BDL_ATTR_SKIP)) g[j] = gpr[e + j];
       float xt = th[j], xg = g[j], xv = v[j], x1 = m1[j], x2 = m2[j];
       update_elem<METHOD, NOISE, COLLECT, RECIP>(a, c, at, xt, xg, xv, t0[j], ep[j], x1, x2);
       if (T::kWriteGrad && gt && !(at & BDL_ATTR_SKIP)) gpr[e + j] = xg;
@@ -754,8 +765,16 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
     if (gi >= gend) continue;
     const int64_t e = gi * 4;
-    const bool gt = a.gbase != nullptr;  // gradient per tensor: element-wise below
+    const bool gt = a.gbase != nullptr;  // gradient per tensor (as in chunk_slow)
     f4v th = ld4(a.theta, e, n), g = gt ? z : ld4(a.grad, e, n), vm = ld4(a.mom, e, n);
+    bool gvec = false;
+    if (gt) {
+      while (rr < a.nruns - 1 && run_end(rr) <= e) ++rr;
+      if (e + 4 <= n && run_end(rr) >= e + 4 && !(run_attr(rr) & kNoFastPath)) {
+        g = vload(run_grad(a, rr) + e);
+        gvec = true;
+      }
+    }
     f4v m = ld4(a.adam_m, e, n), v = ld4(a.adam_v, e, n), t0 = ld4(a.prior_mean, e, n);
     f4v buf = z, ep = z, m1 = z, m2 = z;
     if (!GRADONLY && c.sgd_mom_read) buf = ld4(a.sgd_buf, e, n);
@@ -770,7 +789,7 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
       while (rr < a.nruns - 1 && run_end(rr) <= e + j) ++rr;
       const uint32_t at = run_attr(rr);
       float* gpr = gt ? run_grad(a, rr) : nullptr;
-      if (gt && !(at & BDL_ATTR_SKIP)) g[j] = gpr[e + j];
+      if (gt && !gvec && !(at & BDL_ATTR_SKIP)) g[j] = gpr[e + j];
       float xt = th[j], xg = g[j], xvm = vm[j], xm = m[j], xv = v[j], xb = buf[j];
       float x1 = m1[j], x2 = m2[j];
       if (!(at & BDL_ATTR_SKIP)) {
