@@ -40,17 +40,25 @@ from __future__ import annotations
 import ctypes as C
 import itertools
 import math
+import os
 
 import torch
 
 from . import _lib as L
 
-CHUNK_TARGET = 1 << 30   # chunk size bound: vectors of up to 1 GiB are one chunk
+# chunk size bound: vectors of up to CHUNK_TARGET bytes are one chunk
+# (BDL_CHUNK_MB overrides, for placement A/Bs)
+CHUNK_TARGET = int(os.environ.get("BDL_CHUNK_MB", "1024")) << 20
 ALIGN = 2 << 20          # chunk sizes are multiples of 2 MiB (large-page mappings)
 FAST_PAIR = 0.97         # a pair this much faster than the median pair is worth taking
 SPARE_ROUNDS = 2         # at most this many rounds of extra chunks while none is seen
 COMPOSITES = 6           # full-size candidate assignments timed besides allocation order
-TORCH_PAIRINGS = 3       # (theta, mom) pairings tried among plain torch allocations
+# plain torch allocations competing with the chunk composites: TORCH_VECTORS
+# of them (the roles + extras; BDL_PLACEMENT_TORCH overrides), every unordered
+# pair tried as (theta, mom), up to TORCH_PAIRINGS — consecutive allocations
+# often sit in one physical group, and a few more of them reach the next
+TORCH_EXTRA = int(os.environ.get("BDL_PLACEMENT_TORCH", "2"))
+TORCH_PAIRINGS = 10
 
 _pending = []  # (device index, va, total bytes) whose unmap was deferred (graph capture)
 
@@ -259,7 +267,8 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
         # allocated plainly, with every (theta, mom) pairing among them
         torch_ms = []
         if search and with_torch:
-            tv = [torch.zeros(n, dtype=torch.float32, device=device) for _ in names]
+            tv = [torch.zeros(n, dtype=torch.float32, device=device)
+                  for _ in range(len(names) + max(0, TORCH_EXTRA))]
             pairs = [(it, im)] + [p for p in itertools.combinations(range(len(tv)), 2)
                                   if set(p) != {it, im}]
             for i, j in pairs[:TORCH_PAIRINGS]:
