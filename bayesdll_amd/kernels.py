@@ -298,10 +298,15 @@ _TUNED = {}
 
 def _scratch_launcher(n, dev, method):
     """A closure launching `method`'s production kernel over scratch buffers of
-    n elements (the buffers live as long as the closure)."""
-    from .flat import FlatState
+    n elements (the buffers live as long as the closure).  Large scratch
+    vectors are placed like a chain's own (flat.placed_vectors): on plain
+    allocations that happen to pair slowly, geometries rank differently than
+    on the placed vectors the sampler then sweeps (3 of 38 round-2 bench runs
+    kept a geometry 1.5-3 % slower there than 1 x 4)."""
+    from .flat import PLACEMENT_MIN_ELEMS, FlatState
     st = FlatState.from_segments([("w", (int(n),))], None, device=dev,
-                                 need_prior=method != "csghmc")
+                                 need_prior=method != "csghmc",
+                                 placement=method if int(n) >= PLACEMENT_MIN_ELEMS else None)
     st.theta.zero_()
     if method == "csghmc":
         kw = dict(lrs=(1e-4, 1e-4), noise_scale=(0.0, 0.0), noise_mode=L.NOISE_NONE,
