@@ -6,7 +6,8 @@ those two land on.  For ViT-L/32 the explore sweep runs ~0.95 ms when the
 pair of physical regions is a "fast" pair and ~1.05 ms otherwise; the
 relation is a property of the physical regions (moving a vector by 256 B ...
 1 GB inside its allocation never changes it; regions come in runs of several
-GB), invisible from user space, and torch's allocator hands out whatever
+GB, with more than two levels of pair time), invisible from user space, and
+torch's allocator hands out whatever
 comes next (profiles/round2/placement/, tools/vmm_class_probe.cpp).
 
 How: instead of drawing whole allocations and hoping, each vector is built
@@ -24,11 +25,12 @@ into one virtual range (hipMemMap), so the pairing is chosen chunk by chunk:
      fastest disjoint pairs; theta / momentum from the pairs, the other roles
      from the remaining chunks in allocation order); each is mapped and timed
      at FULL size — chunk-pair times only rank the seeds; and, competing
-     with them, the roles allocated plainly by torch with TORCH_PAIRINGS
-     (theta, mom) pairings among those allocations (on some boxes hipMalloc'd
-     memory pairs faster than any chunk composite).  The fastest is kept; the per-chunk views are unmapped and every handle released
-     (unchosen chunks return to the driver at once — nothing is parked in
-     torch's cache).
+     with them, the roles plus TORCH_EXTRA more vectors allocated plainly by
+     torch, with up to TORCH_PAIRINGS (theta, mom) pairings among them (on
+     some boxes hipMalloc'd memory pairs faster than any chunk composite).
+     The fastest is kept; the per-chunk views are unmapped and every handle
+     released (unchosen chunks return to the driver at once — nothing is
+     parked in torch's cache).
 
 Results never depend on placement (the kernels read the same values from any
 address).  The mapped ranges are exposed to torch through
