@@ -28,6 +28,7 @@ from . import _runner as R
 from . import kernels as K
 from ._base import FusedModelBase
 from .cyclical import CyclicalSGMCMC
+from .flat import moment_pair
 
 
 class Runner:
@@ -154,8 +155,7 @@ class Runner:
         collect mode, buffers and divisor, plus the count to store."""
         st = self.model.state_for(self.net)
         if cycle_number not in self.cycle_theta_mom1:
-            m1 = torch.empty(st.n, dtype=torch.float32, device=st.device)
-            m2 = torch.empty(st.n, dtype=torch.float32, device=st.device)
+            m1, m2 = moment_pair(st.n, st.device)
             self.cycle_theta_mom1[cycle_number] = m1
             self.cycle_theta_mom2[cycle_number] = m2
             return (L.COLLECT_WELFORD_INIT, m1, m2, 1.0), 1

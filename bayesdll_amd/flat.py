@@ -602,6 +602,31 @@ def draw_buffer(out, launch, candidates=DRAW_CANDIDATES):
     return cands[best], [round(t, 4) for t in ms]
 
 
+MOMENT_PAIR_ALIGN = 64  # elements: m2 starts 256 B after a 256-B boundary
+
+
+def moment_pair(n, device):
+    """(m1, m2) for one cycle's Welford / running moments (methods/csghmc.py:333-337,
+    methods/csgld.py:282-293): the two halves of ONE allocation, m2 starting
+    on a 256-B boundary.  Why (DESIGN.md §4 placement): the posterior draw
+    (m1 r, m2 r, out w) runs 0.608-0.616 ms for ViT-L/32 with m1 / m2 in one
+    physical class and out in the other, 0.631-0.650 with m1 / m2 split
+    (profiles/round2/placement/aux_roles/collect_and_sample_by_class.jsonl);
+    one allocation puts both halves in one class, and flat.draw_buffer then
+    picks an output buffer from the other.  The collect steps that fill them
+    do not care (1.754-1.762 ms over all four class combinations).  Vectors
+    below PLACEMENT_MIN_ELEMS, or BDL_PLACEMENT=0: two plain allocations.
+    Values never depend on it; torch.save of both halves in one call stores
+    the shared storage once."""
+    import os
+    f32 = dict(dtype=torch.float32, device=device)
+    if n < PLACEMENT_MIN_ELEMS or os.environ.get("BDL_PLACEMENT", "search") == "0":
+        return torch.empty(n, **f32), torch.empty(n, **f32)
+    stride = -(-n // MOMENT_PAIR_ALIGN) * MOMENT_PAIR_ALIGN
+    buf = torch.empty(stride + n, **f32)
+    return buf[:n], buf[stride:stride + n]
+
+
 def fill_normal_per_tensor(vec, numels, generator=None):
     """Per-tensor normal_() over consecutive slices of `vec` (the reference's
     per-parameter torch.randn_like(p) stream)."""

@@ -198,8 +198,12 @@ def aux_kernels(st, reps=20):
     m1 rw, m2 rw = 20 B/elem)."""
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
+    from bayesdll_amd.flat import draw_buffer, moment_pair
     n = st.n
-    m1, m2, out = (torch.empty(n, dtype=torch.float32, device=st.device) for _ in range(3))
+    # the draw reads a cycle's Welford moments, allocated as the cSGHMC Runner
+    # allocates them (flat.moment_pair: one allocation, two halves)
+    m1, m2 = moment_pair(n, st.device)
+    out = torch.empty(n, dtype=torch.float32, device=st.device)
     m1.copy_(st.theta)
     m2.fill_(1e-6)
     res = {}
@@ -220,15 +224,21 @@ def aux_kernels(st, reps=20):
 
     # the output buffer chosen as the Runners' posterior draws choose it
     # (flat.draw_buffer: the plain allocation first, then fresh ones, timed)
-    from bayesdll_amd.flat import draw_buffer
     out, cand_ms = draw_buffer(out, lambda b: K.posterior_sample(
         b, m1, m2, var_mode=L.VAR_WELFORD, ratio=4.0, seed=7, chain=0, step=0))
     timed("posterior_sample", 12, lambda i: K.posterior_sample(
         out, m1, m2, var_mode=L.VAR_WELFORD, ratio=4.0, seed=7, chain=0, step=i))
     res["posterior_sample"]["out_candidates_ms"] = cand_ms
-    timed("moments_update", 20, lambda i: K.moments_update(
-        st.theta, m1, m2, L.COLLECT_MEAN, collect_a=float(i + 1), collect_b=float(i + 2)))
+    res["posterior_sample"]["moments"] = "flat.moment_pair"
     del m1, m2, out
+    # the running moments of sgld / sghmc (methods/sgld.py:95-102 seeds them
+    # from theta at burn-in): two plain allocations, as the sgld Runner's
+    s1, s2 = (torch.empty(n, dtype=torch.float32, device=st.device) for _ in range(2))
+    s1.copy_(st.theta)
+    s2.fill_(1e-6)
+    timed("moments_update", 20, lambda i: K.moments_update(
+        st.theta, s1, s2, L.COLLECT_MEAN, collect_a=float(i + 1), collect_b=float(i + 2)))
+    del s1, s2
     return res
 
 
@@ -306,7 +316,7 @@ def main():
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
     from bayesdll_amd.cyclical import CyclicalSGMCMC
-    from bayesdll_amd.flat import FlatState
+    from bayesdll_amd.flat import FlatState, moment_pair
     from bayesdll_amd.shapes import segments
 
     segs, readout = segments(a.backbone, a.num_classes)
@@ -369,9 +379,8 @@ def main():
         for k in range(total):
             if sched.should_sample(0, k, total) and k % a.thin == 0:
                 c = sched.get_cycle_number(0, k, total)
-                if c not in pre:
-                    pre[c] = tuple(torch.empty(n, dtype=torch.float32, device=dev)
-                                   for _ in range(2))
+                if c not in pre:  # as the cSGHMC Runner allocates them
+                    pre[c] = moment_pair(n, dev)
     torch.cuda.synchronize()
     moment_buffers = {"cycles": len(pre), "alloc_ms": round((time.perf_counter() - t_alloc) * 1e3, 1)}
     if sgld:  # sgld.py:95-102 burn-in seeding (burnin = 0), outside the timed region

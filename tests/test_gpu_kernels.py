@@ -832,3 +832,36 @@ def test_moments_and_sample_kernels_edge_sizes(n):
     K.posterior_sample(out, a1, None, var_mode=L.VAR_WELFORD, seed=3, chain=1, step=9)
     torch.cuda.synchronize()
     assert torch.equal(out, a1 + torch.full_like(a1, 1e-12).sqrt() * z)
+
+
+def test_moment_pair_changes_nothing_but_the_addresses(monkeypatch):
+    """flat.moment_pair (the cSGHMC Runner's per-cycle Welford buffers, two
+    halves of one allocation at ViT sizes): the fused Welford collect steps and
+    the posterior draws from them equal those into two separate allocations
+    bit for bit."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.flat import FlatState, PLACEMENT_MIN_ELEMS, moment_pair
+    segs = [("l0.weight", (PLACEMENT_MIN_ELEMS + 5,)), ("fc.weight", (1027,))]
+    res = []
+    for place in ("search", "0"):
+        monkeypatch.setenv("BDL_PLACEMENT", place)
+        st = FlatState.from_segments(segs, "fc", device=DEV)
+        m1, m2 = moment_pair(st.n, st.device)
+        paired = m1.untyped_storage().data_ptr() == m2.untyped_storage().data_ptr()
+        assert paired == (place == "search")
+        g = torch.Generator(device=DEV).manual_seed(0)
+        st.theta.normal_(0, 0.02, generator=g)
+        st.grad.normal_(0, 1e-3, generator=g)
+        for k, (collect, cnt) in enumerate(((L.COLLECT_WELFORD_INIT, 1.0), (L.COLLECT_WELFORD, 3.0),
+                                            (L.COLLECT_WELFORD, 5.0))):
+            K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-3, 1e-2), noise_scale=(1e-3, 1e-3),
+                          noise_mode=L.NOISE_PHILOX, one_minus_alpha=0.9, prior_sig=1.0,
+                          collect=collect, mom1=m1, mom2=m2, collect_a=cnt, seed=5, step=k)
+        out = torch.empty(st.n, dtype=torch.float32, device=DEV)
+        K.posterior_sample(out, m1, m2, var_mode=L.VAR_WELFORD, ratio=2.0, seed=7, chain=1, step=3)
+        torch.cuda.synchronize()
+        res.append([t.clone() for t in (st.theta, st.mom, m1, m2, out)])
+        del st, m1, m2, out
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

@@ -84,3 +84,27 @@ def test_draw_buffer_keeps_small_vectors_and_honours_placement_off(monkeypatch):
     out, ms = F.draw_buffer(big, launch)
     assert out is big and ms is None
 
+
+
+def test_moment_pair_halves_of_one_allocation(monkeypatch):
+    """flat.moment_pair: for vectors of >= PLACEMENT_MIN_ELEMS, m1 / m2 are the
+    two halves of one allocation (disjoint, m2 on a 256-B boundary, both
+    contiguous, n elements each); smaller vectors and BDL_PLACEMENT=0 get two
+    plain allocations."""
+    import torch
+
+    from bayesdll_amd import flat as F
+    monkeypatch.delenv("BDL_PLACEMENT", raising=False)
+    for n in (F.PLACEMENT_MIN_ELEMS, F.PLACEMENT_MIN_ELEMS + 3, 306535400):
+        m1, m2 = F.moment_pair(n, "cpu")
+        assert m1.numel() == n and m2.numel() == n
+        assert m1.is_contiguous() and m2.is_contiguous()
+        assert m1.untyped_storage().data_ptr() == m2.untyped_storage().data_ptr()
+        assert m1.data_ptr() + 4 * n <= m2.data_ptr()
+        assert (m2.data_ptr() - m1.data_ptr()) % 256 == 0
+        assert m2.data_ptr() + 4 * n <= m1.untyped_storage().data_ptr() + m1.untyped_storage().nbytes()
+    small = F.moment_pair(1000, "cpu")
+    assert small[0].untyped_storage().data_ptr() != small[1].untyped_storage().data_ptr()
+    monkeypatch.setenv("BDL_PLACEMENT", "0")
+    a, b = F.moment_pair(F.PLACEMENT_MIN_ELEMS, "cpu")
+    assert a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr()
