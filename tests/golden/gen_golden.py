@@ -550,6 +550,18 @@ FULLSIZE_CONFIGS = {
         noise_seed=47,
         hparams=dict(prior_sig=1.0, bias="informative", Ninflate=1e3, nd=0.01, burnin=1,
                      thin=2, nst=2))),
+    # config 4 (the headline): ViT-L/32 (C=1000, 296 tensors, 306,535,400) cSGHMC
+    # with the csghmc hparams of pretrain_resnet101.py:127 (alpha_m 0.18,
+    # nd 0.01, Ninflate 1) and the vision demos' lr 1e-4 / lr_head 1e-2, ND =
+    # Pets trainval x 0.5 (README.md:139).  Two cycles of 10 steps: the
+    # sampling half is one epoch of 5 batches, thin 2 on the batch index
+    # (quirk Q4) -> batches 0, 2, 4 -> Welford init + 2 updates per cycle, the
+    # Q2 doubled count, and each cycle's end (likelihoods + checkpoint).
+    "fullsize_c4_csghmc": ("csghmc", "vit_l_32", 1000, dict(
+        epochs=4, bpe=5, num_cycles=2, beta=0.5, lr=1e-4, lr_head=1e-2, ND=1840, init_seed=48,
+        init_scale=0.02, grad_seed=49, grad_scale=1e-3, noise_seed=50,
+        hparams=dict(prior_sig=1.0, bias="informative", momentum_decay=0.18, Ninflate=1.0,
+                     nd=0.01, burnin=0, thin=2, nst=1))),
 }
 
 
@@ -691,7 +703,10 @@ def main():
         return
     if only == "fullsize":
         torch.set_num_threads(8)
+        pick = os.environ.get("GOLDEN_FULLSIZE")  # comma list; default: every config
         for name, (method, backbone, classes, cfg) in FULLSIZE_CONFIGS.items():
+            if pick and name not in pick.split(","):
+                continue
             rec = run_fullsize(methods, method, backbone, classes, copy.deepcopy(cfg))
             np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **rec)
             print(f"wrote {name}.npz n={int(rec['n'])} draws={int(rec['draws'])} "

@@ -1,11 +1,13 @@
-"""Config-size parity against reference-produced data (SURVEY §8(d) C2, C3).
+"""Config-size parity against reference-produced data (SURVEY §8(d) C2, C3, C4).
 
 tests/golden/gen_golden.py ran the REFERENCE Runners' own step loops
 (methods/csghmc.py:246-384 + :747-778 for C2; methods/sgld.py:193-250 +
 :469-484 + torch SGD(momentum 0.5) + the running moments :236-246 for C3) on a
 FakeNet with the real parameter shapes of the config's backbone — mlp_mnist
-(8 tensors, 2,797,010 params) and ResNet-101 C=1000 (314 tensors, 44,549,160)
-— prescribed gradients and a deterministic per-tensor noise stream in place
+(8 tensors, 2,797,010 params), ResNet-101 C=1000 (314 tensors, 44,549,160) and,
+for the headline C4, ViT-L/32 C=1000 (296 tensors, 306,535,400: two cycles of
+10 steps, Welford init + 2 updates per cycle with the Q2 doubled count, the
+cycle-end likelihood draws) — prescribed gradients and a deterministic per-tensor noise stream in place
 of torch.randn_like.  The fixtures hold a 4096-element index subsample,
 float64 norms and the SHA-256 of the exact fp32 bytes of every final vector.
 
@@ -117,7 +119,7 @@ def replay(fx, div_mode):
     return runner, prov, {k: v.detach().cpu().numpy() for k, v in vecs.items()}
 
 
-@pytest.mark.parametrize("name", ["fullsize_c2_csghmc", "fullsize_c3_sgld"])
+@pytest.mark.parametrize("name", ["fullsize_c2_csghmc", "fullsize_c3_sgld", "fullsize_c4_csghmc"])
 @pytest.mark.parametrize("div_mode", ["true", "recip"])
 def test_config_size_replay_matches_reference(name, div_mode):
     fx = load(name)

@@ -4,6 +4,8 @@ Golden fixtures were produced by running the reference's own Runner/Model code
 (tests/golden/gen_golden.py); here the oracle replays the same prescribed
 gradients and captured noise and must land on identical bits.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -85,12 +87,17 @@ def _fullsize_noise_fn(fx, segments):
                                      for i, n in enumerate(numels)])
 
 
-@pytest.mark.parametrize("name", ["fullsize_c2_csghmc", "fullsize_c3_sgld"])
+@pytest.mark.parametrize("name", [
+    "fullsize_c2_csghmc", "fullsize_c3_sgld",
+    pytest.param("fullsize_c4_csghmc", marks=pytest.mark.skipif(
+        not os.environ.get("BDL_SLOW"),
+        reason="ViT-L/32 size: ~4 min of CPU; set BDL_SLOW=1"))])
 def test_oracle_matches_reference_at_config_size(name):
-    """SURVEY §8(d) C2 (mlp_mnist, 2,797,010 params, cSGHMC) and C3 (ResNet-101
-    C=1000, 44,549,160 params, SGLD + SGD momentum): the oracle run on the
-    real shapes lands on the reference's exact final bytes (SHA-256 of every
-    final vector, tests/golden/gen_golden.py FULLSIZE_CONFIGS)."""
+    """SURVEY §8(d) C2 (mlp_mnist, 2,797,010 params, cSGHMC), C3 (ResNet-101
+    C=1000, 44,549,160 params, SGLD + SGD momentum) and C4 (ViT-L/32 C=1000,
+    306,535,400 params, cSGHMC): the oracle run on the real shapes lands on
+    the reference's exact final bytes (SHA-256 of every final vector,
+    tests/golden/gen_golden.py FULLSIZE_CONFIGS)."""
     import hashlib
     from bayesdll_amd.shapes import segments
     from fakenet import grads_for_step, init_vector
