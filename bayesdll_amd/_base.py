@@ -44,6 +44,8 @@ def release_deferred_graphs():
     if _DEFERRED_GRAPHS and not torch.cuda.is_current_stream_capturing():
         torch.cuda.synchronize()
         _DEFERRED_GRAPHS.clear()
+    from . import placement
+    placement.release_pending()  # chunk mappings whose last tensor died inside a capture
 
 
 def _drop_graphs(graphs):
@@ -147,6 +149,16 @@ class FusedModelBase(nn.Module):
             self.release_graphs()  # graphs captured against the old state's buffers
             if self.noise_mode not in NOISE_MODES:
                 raise ValueError(f"noise_mode must be one of {NOISE_MODES}")
+            # launch geometry for this device and size (speed only: results
+            # never depend on it), tuned BEFORE the chain's vectors exist: the
+            # tuning's scratch vectors are placed with the chain's roles, and
+            # their placed set, parked when they die, becomes the chain's
+            # (bayesdll_amd.placement pool: one placement search, not two)
+            from . import kernels as K
+            params = list(net.parameters())
+            n_all = sum(p.numel() for p in params)
+            launch_cfg = K.autotune_once(n_all, params[0].device, self.tune_method) \
+                if params and params[0].is_cuda else None
             self._state = FlatState(net, net0, readout_name=getattr(net, "readout_name", None),
                                     bias=getattr(self, "bias", "informative"),
                                     need_prior=self.need_prior, need_mom=self.need_mom,
@@ -155,13 +167,8 @@ class FusedModelBase(nn.Module):
             self._state_net = net
             steps_timed = int(os.environ.get("BDL_STEP_TIMING", "0") or 0)
             if steps_timed > 0:  # sampled update timing, logged once per epoch
-                from . import kernels as K
                 self._state.timer = K.StepTimer(steps_timed)
-            # launch geometry for this device and size (speed only: results
-            # never depend on it)
-            from . import kernels as K
-            self._state.launch_cfg = K.autotune_once(self._state.n, self._state.device,
-                                                     self.tune_method)
+            self._state.launch_cfg = launch_cfg
         return self._state
 
     @property

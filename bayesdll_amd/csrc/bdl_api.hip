@@ -1024,17 +1024,24 @@ int bdl_vmm_map(int32_t device, const uint64_t* handles, int32_t nchunks, uint64
   const int rc = hip_fail("bdl_vmm_map: hipMemMap/hipMemSetAccess", e);
   for (int32_t i = 0; i < mapped; ++i)
     (void)hipMemUnmap((char*)base + (size_t)i * chunk_bytes, chunk_bytes);
-  (void)hipMemAddressFree(base, total);
+  // the range stays reserved, as after bdl_vmm_unmap: chunks were mapped into
+  // it, so it must never be handed to other chunks (see below)
   return rc;
 }
 
 // The virtual range stays RESERVED after the unmap, for the life of the
-// process: a range freed with hipMemAddressFree is handed out again by the next
-// reservation, and on this stack the GPU then keeps translating it to the
-// PREVIOUS mapping's physical chunks for a while — writes through the new
-// mapping land in the old (possibly released) memory (tools/vmm_alias_check.py,
-// profiles/round2/vmm/alias_reuse.jsonl).  Never reusing a range costs only
-// virtual address space (a chain state reserves a few tens of GB of it).
+// process.  On this stack a virtual address that has been mapped once keeps
+// translating to its FIRST physical backing after hipMemUnmap: mapping other
+// chunks at that address — after hipMemAddressFree and a new reservation that
+// returns the same address, or re-mapping into the still-reserved range — sends
+// every write through the new mapping into the OLD chunks, with or without a
+// device synchronisation around the unmap and whether the range is unmapped
+// whole or chunk by chunk (tools/vmm_alias_repro.cpp, plain HIP, one scenario
+// per process: profiles/round3/vmm/).  Only a never-mapped address is correct,
+// so no range is ever reused for other chunks; the Python side parks whole
+// placed sets (still mapped) for reuse instead of unmapping them
+// (bayesdll_amd/placement.py), which keeps the reserved address space from
+// growing per chain state.
 int bdl_vmm_unmap(void* va, uint64_t total_bytes) {
   if (!va) return fail(BDL_ERR_NULL, "bdl_vmm_unmap: null va");
   const hipError_t e = hipMemUnmap(va, total_bytes);

@@ -133,11 +133,19 @@ def placed_vectors(n, device, names, method):
     from . import placement as P
     free, _ = torch.cuda.mem_get_info(device)
     runs_by_n = {}
+    # the gradient is read-only in every sweep and its placement never shows
+    # (profiles/round2/placement/role_mix/): a plain allocation, outside the
+    # placed set, so the set's key does not depend on the gradient mode (a
+    # "tensor"-mode state drops it at once)
+    pnames = [nm for nm in names if nm != "grad"]
+    grad = torch.zeros(n, **f32) if "grad" in names else None
+    per, cb = P.chunk_geometry(n)
+    gsrc = grad if grad is not None and cb // 4 <= n else torch.zeros(max(n, cb // 4), **f32)
 
     def launcher(roles, m):
         if m not in runs_by_n:
             runs_by_n[m] = build_runs([0], [m], [L.ATTR_PRIOR], m).to(device)
-        return _placement_launcher(method, roles, m, device, runs_by_n[m])
+        return _placement_launcher(method, dict(roles, grad=gsrc[:m]), m, device, runs_by_n[m])
 
     from . import kernels as K
     # the probe kernel's depth is fixed at 4; workgroups per CU: the method's
@@ -147,8 +155,9 @@ def placed_vectors(n, device, names, method):
     bpc = int(os.environ.get("BDL_PLACEMENT_BPC", "0")) or PLACEMENT_BPC.get(method, 1)
     prev = K.set_launch_config(bpc, 4, 1)
     try:
-        vecs, info = P.place(n, device, names, launcher, lambda f: _time_launch(f, device, 5),
-                             budget_bytes=int(0.25 * free), search=mode == "search")
+        vecs, info = P.place(n, device, pnames, launcher, lambda f: _time_launch(f, device, 5),
+                             budget_bytes=int(0.25 * free), search=mode == "search",
+                             pool_key=(method, bpc))
     except RuntimeError as e:  # chunk mappings unavailable: plain allocations
         import warnings
         warnings.warn(f"bayesdll_amd: physical-chunk placement unavailable ({e}); "
@@ -157,8 +166,51 @@ def placed_vectors(n, device, names, method):
                                                              "error": str(e)[:200]}
     finally:
         K.restore_launch_config(prev)
-    info["method"] = method
+        del gsrc
+    info = dict(info, method=method)
+    if grad is not None:
+        vecs["grad"] = grad
     return vecs, info
+
+
+def placed_moments(theta, need_m2=True):
+    """(m1, m2) running-moment vectors of theta's size for the stand-alone
+    bdl_moments_update sweep (methods/sgld.py:95-102 seeding, :236-246 the
+    running mean; theta r, m1 rw, m2 rw), zeroed, placed the way the step's
+    theta / mom pair is: that sweep is fast iff its two read-modify-write
+    streams m1 / m2 sit in different physical groups (DESIGN.md §4,
+    profiles/round2/placement/aux_roles/: 0.965-0.973 vs 1.04-1.08 ms for
+    ViT-L/32), so the pair is built from physical chunks whose pairings are
+    timed with the moments kernel itself (bayesdll_amd.placement, roles
+    theta -> m1, mom -> m2; plain torch allocations compete).  Below
+    PLACEMENT_MIN_ELEMS, without m2, or with BDL_PLACEMENT=0: plain
+    allocations.  Values never depend on it.  Returns (m1, m2, info)."""
+    import os
+    n, device = theta.numel(), theta.device
+    mode = os.environ.get("BDL_PLACEMENT", "search")
+    if not need_m2 or n < PLACEMENT_MIN_ELEMS or mode == "0":
+        return (torch.zeros_like(theta), torch.zeros_like(theta) if need_m2 else None, None)
+    from . import kernels as K
+    from . import placement as P
+
+    def launcher(roles, m):
+        k = min(m, n)  # a one-chunk vector's chunk is rounded up past n
+        src, m1, m2 = theta[:k], roles["theta"][:k], roles["mom"][:k]
+        return lambda: K.moments_update(src, m1, m2, L.COLLECT_MEAN, collect_a=3.0,
+                                        collect_b=4.0)
+
+    free, _ = torch.cuda.mem_get_info(device)
+    try:
+        vecs, info = P.place(n, device, ["theta", "mom"], launcher,
+                             lambda f: _time_launch(f, device, 5), budget_bytes=int(0.25 * free),
+                             search=mode == "search", pool_key=("moments",))
+    except RuntimeError as e:  # chunk mappings unavailable: plain allocations
+        import warnings
+        warnings.warn(f"bayesdll_amd: physical-chunk placement unavailable ({e}); "
+                      "using torch's allocator")
+        return torch.zeros_like(theta), torch.zeros_like(theta), {"allocator": "torch",
+                                                                  "error": str(e)[:200]}
+    return vecs["theta"], vecs["mom"], dict(info, method="moments")
 
 
 GRAD_MODES = ("tensor", "flat")

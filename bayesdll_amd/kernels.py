@@ -296,6 +296,9 @@ AUTOTUNE_CANDIDATES = ((2, 1, 1), (1, 4, 1), (3, 1, 1), (2, 4, 1), (1, 2, 1), (2
 _TUNED = {}
 
 
+ADAM_EXTRA = ("adam_m", "adam_v", "sgd_buf")  # adam_sghmc.Model.extra_vectors
+
+
 def _scratch_launcher(n, dev, method):
     """A closure launching `method`'s production kernel over scratch buffers of
     n elements (the buffers live as long as the closure).  Large scratch
@@ -304,9 +307,13 @@ def _scratch_launcher(n, dev, method):
     on the placed vectors the sampler then sweeps (3 of 38 round-2 bench runs
     kept a geometry 1.5-3 % slower there than 1 x 4)."""
     from .flat import PLACEMENT_MIN_ELEMS, FlatState
+    # the same roles as the sampler's own state, so that its placed set, parked
+    # when this scratch state dies, is the one the sampler's state then takes
+    # (bayesdll_amd.placement pool: one search per process and size)
     st = FlatState.from_segments([("w", (int(n),))], None, device=dev,
                                  need_prior=method != "csghmc",
-                                 placement=method if int(n) >= PLACEMENT_MIN_ELEMS else None)
+                                 placement=method if int(n) >= PLACEMENT_MIN_ELEMS else None,
+                                 extra=ADAM_EXTRA if method == "adam" else ())
     st.theta.zero_()
     if method == "csghmc":
         kw = dict(lrs=(1e-4, 1e-4), noise_scale=(0.0, 0.0), noise_mode=L.NOISE_NONE,
@@ -323,9 +330,7 @@ def _scratch_launcher(n, dev, method):
             sgmcmc_step(st, L.SGLD, **kw)
     elif method == "adam":
         st.prior.zero_()
-        m = torch.zeros_like(st.theta)
-        v = torch.zeros_like(st.theta)
-        buf = torch.zeros_like(st.theta)
+        m, v, buf = (st.extra[k] for k in ADAM_EXTRA)
         kw = dict(adam_m=m, adam_v=v, sgd_buf=buf, beta1=0.9, beta2=0.999, eps=1e-8, t=3,
                   momentum_decay=0.1, nd=0.01, lrs=(1e-4, 1e-4), noise_mode=L.NOISE_PHILOX,
                   sigma2=1.0, n_data=1e6, mu=0.5, momentum=True)
@@ -383,6 +388,8 @@ def autotune(n, device=None, reps=6, candidates=None, method="csghmc"):
     best = min(top, key=times.get)
     set_launch_config(*best)
     del launch
+    import gc
+    gc.collect()  # the scratch state now, so that its placed set is parked for the chain
     torch.cuda.empty_cache()
     return best, times
 

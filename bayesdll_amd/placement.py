@@ -34,9 +34,26 @@ into one virtual range (hipMemMap), so the pairing is chosen chunk by chunk:
 
 Results never depend on placement (the kernels read the same values from any
 address).  The mapped ranges are exposed to torch through
-__cuda_array_interface__; a range is unmapped when the last tensor viewing it
-is freed — after a device synchronisation, and never inside a HIP-graph
-capture (it is then queued and unmapped at the next release point)."""
+__cuda_array_interface__.
+
+Virtual ranges are never handed to a second set of chunks: on this stack a
+virtual address that has once been mapped keeps translating to its FIRST
+physical backing after hipMemUnmap, whatever the synchronisation, the unmap
+granularity, or whether the range was freed and re-reserved or kept and
+re-mapped (tools/vmm_alias_repro.cpp, profiles/round3/vmm/: every scenario
+that maps other chunks at a used address writes the OLD chunks; only a
+never-used address is correct).  So an unmapped range stays reserved for the
+life of the process (bdl_vmm_unmap), and to keep that address space from
+growing with every chain state, the kept vectors of a placement are a
+PlacedSet: when the last tensor of the set dies the set is PARKED — still
+mapped, physical memory kept, like a block in torch's caching allocator — and
+the next placement with the same key (device, size, roles, method) takes it
+back as is: same chunks, same addresses, already searched.  Parked sets of
+other keys are unmapped when a new search starts (their memory is then
+needed); `release_pool()` unmaps all of them.  A range that is not part of a
+set (candidates that lost, per-chunk views) is unmapped when its last tensor
+goes — after a device synchronisation, and never inside a HIP-graph capture
+(it is then queued and unmapped at the next release point)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -58,17 +75,42 @@ COMPOSITES = 6           # full-size candidate assignments timed besides allocat
 # plain torch allocations competing with the chunk composites: TORCH_VECTORS
 # of them (the roles + extras; BDL_PLACEMENT_TORCH overrides), every unordered
 # pair tried as (theta, mom), up to TORCH_PAIRINGS — consecutive allocations
-# often sit in one physical group, and a few more of them reach the next
+# often sit in one physical group, and a few more of them reach the next;
+# negative: no torch competitors (chunk composites only)
 TORCH_EXTRA = int(os.environ.get("BDL_PLACEMENT_TORCH", "2"))
 TORCH_PAIRINGS = 10
 
+# parked PlacedSets per key, and the bytes they hold (BDL_PLACEMENT_POOL_GB caps
+# them per process; 0 disables parking)
+POOL_MAX_BYTES = int(float(os.environ.get("BDL_PLACEMENT_POOL_GB", "64")) * (1 << 30))
+_POOL = {}
+_POOL_BYTES = [0]
+_VA_RESERVED = [0]  # bytes of virtual address space this process reserved for mappings
+
 _pending = []  # (device index, va, total bytes) whose unmap was deferred (graph capture)
+
+
+def va_reserved_bytes():
+    """Virtual address space reserved by this process's mappings so far (never
+    returned: see the module docstring)."""
+    return _VA_RESERVED[0]
+
+
+def pooled_bytes():
+    return _POOL_BYTES[0]
 
 
 def _unmap_now(dev_index, va, total):
     with torch.cuda.device(dev_index):
         torch.cuda.synchronize()
     L.check(L.lib().bdl_vmm_unmap(C.c_void_p(va), total), "bdl_vmm_unmap")
+
+
+def _unmap_or_defer(dev_index, va, total):
+    if torch.cuda.is_current_stream_capturing():
+        _pending.append((dev_index, va, total))
+    else:
+        _unmap_now(dev_index, va, total)
 
 
 def release_pending():
@@ -79,20 +121,90 @@ def release_pending():
         _unmap_now(*_pending.pop())
 
 
+def release_pool(keep_key=None):
+    """Unmap every parked set (their physical memory returns to the driver;
+    the virtual ranges stay reserved), except those of `keep_key`."""
+    for key in list(_POOL):
+        if key == keep_key:
+            continue
+        for ps in _POOL.pop(key):
+            _POOL_BYTES[0] -= ps.nbytes()
+            for va, total in ps.back.values():
+                _unmap_or_defer(ps.dev_index, va, total)
+
+
+class PlacedSet:
+    """The kept vectors of one placement (role -> mapped range).  While any of
+    them lives, all stay mapped; when the last dies the set is parked in the
+    pool (or unmapped when parking is off / over the cap)."""
+
+    def __init__(self, key, dev_index, info):
+        self.key, self.dev_index, self.info = key, dev_index, info
+        self.roles = {}  # role -> (va, total) of the live mappings
+        self.back = {}   # role -> (va, total) of the mappings whose tensors died
+
+    def adopt(self, role, mapping):
+        mapping.owner, mapping.role = self, role
+        self.roles[role] = (mapping.va, mapping.total)
+
+    def nbytes(self):
+        return sum(t for _, t in self.roles.values())
+
+    def give_back(self, role, va, total):
+        """Called from Mapping.__del__; True when the range was taken care of."""
+        self.back[role] = (va, total)
+        if len(self.back) < len(self.roles):
+            return True  # others of the set still alive: stay mapped
+        nb = self.nbytes()
+        if self.key is not None and _POOL_BYTES[0] + nb <= POOL_MAX_BYTES:
+            _POOL.setdefault(self.key, []).append(self)
+            _POOL_BYTES[0] += nb
+            return True
+        for v, t in self.back.values():
+            _unmap_or_defer(self.dev_index, v, t)
+        return True
+
+
+def take_parked(key, n):
+    """A parked set for `key`, re-exposed as fresh tensors over the same
+    mappings (no map call), or None."""
+    sets = _POOL.get(key)
+    if not sets:
+        return None
+    old = sets.pop()
+    if not sets:
+        del _POOL[key]
+    _POOL_BYTES[0] -= old.nbytes()
+    with torch.cuda.device(old.dev_index):
+        torch.cuda.synchronize()  # work on the dead tensors is finished
+    ps = PlacedSet(key, old.dev_index, old.info)
+    vecs = {}
+    for role, (va, total) in old.back.items():
+        m = Mapping(old.dev_index, None, None, n, adopt=(va, total))
+        ps.adopt(role, m)
+        vecs[role] = m.tensor()
+    return vecs, ps
+
+
 class Mapping:
     """One contiguous virtual range mapped from physical chunks (bdl_vmm_map),
     seen by torch as a flat fp32 tensor.  Torch's tensor keeps this object
     alive (from_blob with a reference to it); when it goes, the range is
     unmapped."""
 
-    def __init__(self, dev_index, handles, chunk_bytes, nelem):
-        arr = (C.c_uint64 * len(handles))(*handles)
-        va = C.c_void_p()
-        L.check(L.lib().bdl_vmm_map(dev_index, arr, len(handles), chunk_bytes, C.byref(va)),
-                "bdl_vmm_map")
+    def __init__(self, dev_index, handles, chunk_bytes, nelem, adopt=None):
+        self.owner, self.role = None, None
         self.dev_index = dev_index
-        self.va = int(va.value)
-        self.total = len(handles) * int(chunk_bytes)
+        if adopt is None:
+            arr = (C.c_uint64 * len(handles))(*handles)
+            va = C.c_void_p()
+            L.check(L.lib().bdl_vmm_map(dev_index, arr, len(handles), chunk_bytes, C.byref(va)),
+                    "bdl_vmm_map")
+            self.va = int(va.value)
+            self.total = len(handles) * int(chunk_bytes)
+            _VA_RESERVED[0] += self.total
+        else:  # a parked set's range, still mapped
+            self.va, self.total = int(adopt[0]), int(adopt[1])
         if nelem * 4 > self.total:
             raise ValueError("bayesdll_amd.placement: mapping smaller than its tensor")
         self.__cuda_array_interface__ = {"shape": (int(nelem),), "typestr": "<f4",
@@ -110,6 +222,9 @@ class Mapping:
         if not va:
             return
         try:
+            owner = self.owner
+            if owner is not None and owner.give_back(self.role, va, self.total):
+                return
             if torch.cuda.is_current_stream_capturing():
                 _pending.append((self.dev_index, va, self.total))
             else:
@@ -203,22 +318,40 @@ def candidate_assignments(times, nchunks, names, per, limit=COMPOSITES):
 
 
 def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, search=True,
-          with_torch=True):
+          with_torch=True, pool_key=None):
     """Allocate `names` (fp32, n elements each, zeroed) from physical chunks,
     theta / mom paired fast.  `launcher(roles: {name: tensor}, n)` returns a
     zero-argument launch of the sampler's kernel; `time_launch(launch)` its
     median ms.  search=False: chunks mapped in allocation order, no pair
-    timing.  Returns ({name: tensor}, info)."""
+    timing.  `pool_key`: the kept vectors form a PlacedSet parked under this
+    key when they die, and a set parked under it is reused instead of a new
+    search.  Returns ({name: tensor}, info)."""
     import time
     t_start = time.perf_counter()
     dev_index = torch.device(device).index
     if dev_index is None:
         dev_index = torch.cuda.current_device()
+    key = None if pool_key is None else (dev_index, int(n), tuple(names), search, pool_key)
+    got = take_parked(key, n) if key is not None else None
+    if got is not None:
+        vecs, ps = got
+        for v in vecs.values():
+            v.zero_()
+        info = dict(ps.info, reused=True, seconds=round(time.perf_counter() - t_start, 3),
+                    search_seconds=ps.info["seconds"], va_reserved_gb=round(_VA_RESERVED[0] / 2**30, 1))
+        return vecs, info
+    release_pool()  # parked sets of other keys: their memory is needed now
     per, cb = chunk_geometry(n)
     nchunk = cb // 4
     nroles = len(names)
     it, im = names.index("theta"), names.index("mom")
     spare = (2 * per if spare is None else spare) if search else 0
+    # footprint up front (ADVICE r2): the chunks and the torch competitors are
+    # alive together; drop the competition, then the spares, if over budget
+    if TORCH_EXTRA < 0 or (nroles * per + spare) * cb + (nroles + TORCH_EXTRA) * 4 * n > budget_bytes:
+        with_torch = False
+    if (nroles * per + spare) * cb > budget_bytes:
+        spare = 0
     ch = _Chunks(dev_index, cb)
     try:
         ch.add(nroles * per + spare)
@@ -249,20 +382,21 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
             rounds += 1
 
         def composite(assign):
-            return {nm: Mapping(dev_index, [ch.handles[k] for k in ids], cb, n).tensor()
+            maps = {nm: Mapping(dev_index, [ch.handles[k] for k in ids], cb, n)
                     for nm, ids in assign.items()}
+            return maps, {nm: m.tensor() for nm, m in maps.items()}
 
         cands = candidate_assignments(times, len(ch.views), names, per)
-        best, best_ms, comp_ms, best_src = None, None, [], None
+        best, best_ms, comp_ms, best_src, best_maps = None, None, [], None, None
         for c in cands:
-            vec = composite(c)
+            maps, vec = composite(c)
             for v in vec.values():
                 v.zero_()
             ms = time_launch(launcher(vec, n))
             comp_ms.append(round(ms, 4))
             if best_ms is None or ms < best_ms:
-                best, best_ms, chosen, best_src = vec, ms, c, "chunks"
-            del vec
+                best, best_ms, chosen, best_src, best_maps = vec, ms, c, "chunks", maps
+            del vec, maps
         ms_d = comp_ms[0]
         # torch's own allocations compete too (on some boxes hipMalloc'd
         # memory pairs faster than any chunk composite): the roles' vectors
@@ -287,7 +421,7 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
                 ms = time_launch(launcher(vec, n))
                 torch_ms.append(round(ms, 4))
                 if ms < best_ms:
-                    best, best_ms, best_src = vec, ms, "torch"
+                    best, best_ms, best_src, best_maps = vec, ms, "torch", None
                     chosen = {nm: [] for nm in names}
             del tv
         keep = best
@@ -309,5 +443,11 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
             "composites_ms": comp_ms, "torch_ms": torch_ms,
             "kept": best_src if best_src == "torch" else
             ("default" if chosen is cands[0] else "search"),
-            "theta_chunks": th_ids, "mom_chunks": mom_ids}
+            "theta_chunks": th_ids, "mom_chunks": mom_ids, "reused": False,
+            "va_reserved_gb": round(_VA_RESERVED[0] / 2**30, 1)}
+    if best_maps is not None and key is not None:
+        ps = PlacedSet(key, dev_index, info)
+        for nm, m in best_maps.items():
+            ps.adopt(nm, m)
+    del best_maps
     return keep, info

@@ -198,7 +198,7 @@ def aux_kernels(st, reps=20):
     m1 rw, m2 rw = 20 B/elem)."""
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
-    from bayesdll_amd.flat import draw_buffer, moment_pair
+    from bayesdll_amd.flat import draw_buffer, moment_pair, placed_moments
     n = st.n
     # the draw reads a cycle's Welford moments, allocated as the cSGHMC Runner
     # allocates them (flat.moment_pair: one allocation, two halves)
@@ -232,12 +232,17 @@ def aux_kernels(st, reps=20):
     res["posterior_sample"]["moments"] = "flat.moment_pair"
     del m1, m2, out
     # the running moments of sgld / sghmc (methods/sgld.py:95-102 seeds them
-    # from theta at burn-in): two plain allocations, as the sgld Runner's
-    s1, s2 = (torch.empty(n, dtype=torch.float32, device=st.device) for _ in range(2))
+    # from theta at burn-in), allocated as the sgld Runner allocates them:
+    # placed for this sweep (flat.placed_moments)
+    s1, s2, pinfo = placed_moments(st.theta)
     s1.copy_(st.theta)
     s2.fill_(1e-6)
     timed("moments_update", 20, lambda i: K.moments_update(
         st.theta, s1, s2, L.COLLECT_MEAN, collect_a=float(i + 1), collect_b=float(i + 2)))
+    if pinfo is not None:
+        res["moments_update"]["placement"] = {k: pinfo.get(k) for k in (
+            "allocator", "kept", "seconds", "default_ms", "chosen_ms", "untuned_torch_ms",
+            "composites_ms", "torch_ms", "pairs_timed")}
     del s1, s2
     return res
 

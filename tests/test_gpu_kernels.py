@@ -634,9 +634,11 @@ def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
             info = st.placement_info
             per, cb = P.chunk_geometry(st.n)
             assert info["chunks_per_vector"] == per == 1
-            assert info["chunks_allocated"] >= 3 * per + 2 * per
+            # the placed set is theta + mom; the read-only gradient is a plain allocation
+            assert info["chunks_allocated"] >= 2 * per + 2 * per
             assert info["pairs_timed"] == info["chunks_allocated"] * (info["chunks_allocated"] - 1)
-            assert len(info["torch_ms"]) == P.TORCH_PAIRINGS
+            nt = 2 + P.TORCH_EXTRA
+            assert len(info["torch_ms"]) == min(P.TORCH_PAIRINGS, nt * (nt - 1) // 2)
             assert len(info["composites_ms"]) >= 2
             assert info["chosen_ms"] == min(info["composites_ms"] + info["torch_ms"])
             assert info["chosen_ms"] <= info["default_ms"]
@@ -648,6 +650,7 @@ def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
             for v in (st.theta, st.grad, st.mom):
                 assert v.is_cuda and v.numel() == st.n
                 assert not v.any()  # zeroed
+            for v in (st.theta, st.mom):
                 if info["kept"] != "torch":
                     assert v.data_ptr() % (2 << 20) == 0
         g = torch.Generator(device=DEV).manual_seed(0)
@@ -739,6 +742,98 @@ def test_composites_mapped_one_after_another_do_not_alias():
             del a, b
     finally:
         ch.release()
+
+
+def test_placed_sets_are_parked_and_reused_without_new_address_space(monkeypatch):
+    """A chain state's placed vectors form a set that is parked, still mapped,
+    when its last tensor dies, and the next state of the same size, roles and
+    method takes it back: same addresses, no new virtual range, no new search,
+    zeroed, and the update gives the same bits (virtual ranges can never be
+    handed to other chunks on this stack: tools/vmm_alias_repro.cpp).  A
+    search for another key unmaps the parked sets first."""
+    import gc
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd import placement as P
+    from bayesdll_amd.flat import FlatState, PLACEMENT_MIN_ELEMS
+    P.release_pool()
+    monkeypatch.setattr(P, "TORCH_EXTRA", -1)  # chunk composites only: a mapped set to park
+    segs = [("l0.weight", (PLACEMENT_MIN_ELEMS + 5,)), ("fc.weight", (1000,))]
+
+    def run(st):
+        g = torch.Generator(device=DEV).manual_seed(3)
+        st.theta.normal_(0, 0.02, generator=g)
+        st.grad.normal_(0, 1e-3, generator=g)
+        for k in range(2):
+            K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-3, 1e-2), noise_scale=(1e-3, 1e-3),
+                          noise_mode=L.NOISE_PHILOX, one_minus_alpha=0.9, prior_sig=1.0,
+                          seed=9, step=k)
+        torch.cuda.synchronize()
+        return st.theta.clone(), st.mom.clone()
+
+    st = FlatState.from_segments(segs, "fc", device=DEV, placement="csghmc")
+    info0 = st.placement_info
+    assert info0["allocator"] == "vmm" and not info0["reused"]
+    ptrs = (st.theta.data_ptr(), st.mom.data_ptr())
+    ref = run(st)
+    va0 = P.va_reserved_bytes()
+    del st
+    gc.collect()
+    assert P.pooled_bytes() > 0
+    for _ in range(3):
+        st = FlatState.from_segments(segs, "fc", device=DEV, placement="csghmc")
+        info = st.placement_info
+        assert info["reused"] and info["chosen_ms"] == info0["chosen_ms"]
+        assert (st.theta.data_ptr(), st.mom.data_ptr()) == ptrs
+        assert not st.mom.any()
+        out = run(st)
+        assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1])
+        assert P.va_reserved_bytes() == va0  # no new address space per state
+        del st, out
+        gc.collect()
+    # a parameter view keeps the set alive (not parked) until it goes too
+    st = FlatState.from_segments(segs, "fc", device=DEV, placement="csghmc")
+    keep = st.theta[:10]
+    del st
+    gc.collect()
+    assert P.pooled_bytes() == 0
+    del keep
+    gc.collect()
+    assert P.pooled_bytes() > 0
+    # another key: the parked set is unmapped before its search
+    st2 = FlatState.from_segments(segs[:1], None, device=DEV, placement="csghmc")
+    assert not st2.placement_info["reused"]
+    assert P.pooled_bytes() == 0
+    del st2
+    gc.collect()
+    P.release_pool()
+
+
+def test_placed_moments_change_nothing_but_the_addresses():
+    """flat.placed_moments (the sgld / sghmc running moments, placed for the
+    stand-alone moments sweep): same bits as plain allocations through the
+    seeding and two running-mean updates (methods/sgld.py:95-102, :236-246)."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.flat import PLACEMENT_MIN_ELEMS, placed_moments
+    n = PLACEMENT_MIN_ELEMS + 7
+    g = torch.Generator(device=DEV).manual_seed(4)
+    thetas = [torch.randn(n, device=DEV, generator=g) for _ in range(3)]
+    outs = []
+    for placed in (False, True):
+        if placed:
+            m1, m2, info = placed_moments(thetas[0])
+            assert info is not None and info["method"] == "moments"
+            assert not m1.any() and not m2.any() and m1.numel() == m2.numel() == n
+        else:
+            m1, m2 = torch.empty(n, device=DEV), torch.empty(n, device=DEV)
+        K.moments_update(thetas[0], m1, m2, L.COLLECT_MEAN_INIT)
+        for k, th in enumerate(thetas[1:], start=1):
+            K.moments_update(th, m1, m2, L.COLLECT_MEAN, collect_a=float(k), collect_b=float(k + 1))
+        torch.cuda.synchronize()
+        outs.append((m1.clone(), m2.clone()))
+        del m1, m2
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
 def test_full_size_vit_csghmc_sample_and_welford_collect_bitexact():
