@@ -198,18 +198,51 @@ def load_checkpoint(path, device):
         return torch.load(path, map_location=device, weights_only=True)
 
 
+def shard_loader(loader, r, k):
+    """Shard r of k of a training loader for a data-parallel likelihood pass,
+    split by SAMPLE index so that the k shards partition the data set whatever
+    order each rank's loader would draw (the reference's train loader
+    shuffles, datasets.py:45-46, and every chain seeds its own generator):
+      * a torch DataLoader over a map-style data set: a DataLoader over the
+        samples r, r + k, ... (same batch size, collate_fn, workers, pinning;
+        no shuffling — the loss sum does not depend on the order);
+      * a list / tuple of batches (identical on every rank): the batches whose
+        index is r mod k;
+    anything else (an iterable data set, a custom batch sampler, drop_last —
+    which drops samples that depend on the shuffle) is refused."""
+    if k == 1:
+        return loader
+    from torch.utils.data import DataLoader, IterableDataset, Subset
+    if isinstance(loader, DataLoader):
+        ds = loader.dataset
+        if isinstance(ds, IterableDataset) or not hasattr(ds, "__len__"):
+            raise ValueError("a sharded likelihood pass needs a map-style data set")
+        if loader.batch_size is None:
+            raise ValueError("a sharded likelihood pass needs a DataLoader with a batch_size "
+                             "(not a custom batch_sampler)")
+        if loader.drop_last:
+            raise ValueError("a sharded likelihood pass cannot reproduce drop_last (which samples "
+                             "are dropped depends on each rank's shuffle)")
+        return DataLoader(Subset(ds, range(r, len(ds), k)), batch_size=loader.batch_size,
+                          shuffle=False, num_workers=loader.num_workers,
+                          collate_fn=loader.collate_fn, pin_memory=loader.pin_memory)
+    if isinstance(loader, (list, tuple)):
+        return [b for i, b in enumerate(loader) if i % k == r]
+    raise ValueError(f"a sharded likelihood pass needs a DataLoader or a list of batches, "
+                     f"got {type(loader).__name__}")
+
+
 def loss_sums(net, loader, criterion, device, shard=(0, 1)):
     """Sum of per-batch mean loss x batch size over `loader` (the reference's
     `loss += loss_.item() * len(y)`, methods/csghmc.py:620-627), accumulated
     on the device in float64 — the same float64 operations in the same order,
-    without a host synchronisation per batch.  shard=(r, k): only batches
-    whose index is r mod k are scored.  Returns (device float64 sum, count)."""
+    without a host synchronisation per batch.  shard=(r, k): only shard r of
+    k of the loader is scored (shard_loader).  Returns (device float64 sum,
+    count)."""
     r, k = shard
     acc = torch.zeros((), dtype=torch.float64, device=device)
     nb = 0
-    for i, (x, y) in enumerate(loader):
-        if i % k != r:
-            continue
+    for x, y in shard_loader(loader, r, k):
         x, y = x.to(device), y.to(device)
         acc = add_loss(acc, criterion(net(x), y), len(y))
         nb += len(y)
@@ -254,11 +287,12 @@ def full_batch_likelihoods(runner, train_loader, mean, m2, var_mode, ratio, thet
 
     group (a torch.distributed process group, or dist.group.WORLD): a
     data-parallel pass — every rank of the group draws the SAME samples (the
-    group's first rank's Philox key; the moments must agree, checked) and
-    scores only the batches whose index is its group rank mod the group size;
-    ONE all_reduce of the [draws, 2] float64 (loss sum, count) table combines
-    them.  The loss sums equal the single-process ones up to the float64
-    summation order."""
+    group's first rank's Philox key; the moments — with nst = 0 the current
+    theta — must agree, checked) and scores only its shard of the training
+    set, split by sample index (shard_loader); ONE all_reduce of the
+    [draws, 2] float64 (loss sum, count) table combines them.  The loss sums
+    equal the single-process ones up to the float64 summation order (and the
+    per-batch float32 means, whose batches differ)."""
     import torch.distributed as dist
     device = runner.args.device
     model = runner.model
@@ -269,7 +303,8 @@ def full_batch_likelihoods(runner, train_loader, mean, m2, var_mode, ratio, thet
             raise ValueError("a sharded likelihood pass needs noise_mode='philox' (the draws must "
                              "be a function of the group's common key)")
         shard = _group_rank_size(group)
-        _check_same_posterior(group, mean.device, mean, m2)
+        # nst = 0 scores the current theta: it must be the same on every rank too
+        _check_same_posterior(group, mean.device, mean, m2, theta if runner.nst == 0 else None)
         key = torch.tensor([seed & ((1 << 63) - 1), chain], dtype=torch.int64,
                            device=mean.device)
         src = dist.get_global_rank(group, 0) if group is not dist.group.WORLD else 0

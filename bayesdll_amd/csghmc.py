@@ -13,6 +13,12 @@ kernel applies, over the flat chain state,
 branches, theta0 is never read) and, on sample steps, the Welford update of the
 current cycle's moments on the new theta (methods/csghmc.py:327-345) in the
 same sweep: 20 B/element on explore steps, 36 B/element on collect steps.
+
+Reproducibility: the fused update gives the same bits in any process for the
+same inputs and Philox key; the gradients come from PyTorch-ROCm autograd,
+whose kernel choice for a shape can depend on what the process ran before.
+A chain repeats bit for bit across processes with deterministic convolutions,
+the math attention backend and a fresh process per chain.
 """
 from __future__ import annotations
 

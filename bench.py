@@ -132,14 +132,19 @@ def _free_port():
     return port
 
 
-def launch_ranks(n):
+def launch_ranks(n, cmd=None, kill_after=20.0):
     """`python bench.py --gpus N` without an outside launcher: start N rank
-    processes of this same command (RANK / LOCAL_RANK / WORLD_SIZE, rendezvous
-    on 127.0.0.1), one per GPU, before this process touches the GPU; wait for
-    all of them and return the first non-zero exit status (the others are
-    stopped), else 0.  Rank 0 prints the JSON line."""
+    processes of this same command (`cmd`, default this script with this
+    process's arguments; RANK / LOCAL_RANK / WORLD_SIZE, rendezvous on
+    127.0.0.1), one per GPU, before this process touches the GPU; wait for all
+    of them and return the first non-zero exit status, else 0.  When one rank
+    fails the others could never pass their barrier: they get SIGTERM, and
+    SIGKILL `kill_after` seconds later if still running.  Rank 0 prints the
+    JSON line."""
     import signal
     import subprocess
+    if cmd is None:
+        cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
     port = str(_free_port())
     procs = []
     for r in range(n):
@@ -147,9 +152,8 @@ def launch_ranks(n):
                    LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=port)
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
-                                      env=env))
-    rc = 0
+        procs.append(subprocess.Popen(cmd, env=env))
+    rc, deadline = 0, None
     pending = list(procs)
     while pending:
         for p in list(pending):
@@ -161,6 +165,11 @@ def launch_ranks(n):
                 rc = code
                 for q in pending:  # one rank failed: the barrier would never complete
                     q.send_signal(signal.SIGTERM)
+                deadline = time.monotonic() + kill_after
+        if deadline is not None and pending and time.monotonic() > deadline:
+            for q in pending:
+                q.kill()
+            deadline = None
         time.sleep(0.05)
     return rc
 

@@ -34,3 +34,60 @@ def test_self_launch_starts_n_ranks_and_propagates_failure():
     assert p.returncode != 0
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert "No HIP GPUs" in p.stderr  # a rank started and failed; the others were stopped
+
+
+RANK_SCRIPT = r"""
+import json, os, signal, sys, time
+out = sys.argv[1]
+r = int(os.environ["RANK"])
+with open(os.path.join(out, f"rank{r}.json"), "w") as f:
+    json.dump({k: os.environ[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                          "MASTER_PORT")}, f)
+if r == int(os.environ["FAIL_RANK"]):
+    time.sleep(0.5)
+    sys.exit(7)
+if os.environ.get("IGNORE_TERM"):
+    signal.signal(signal.SIGTERM, signal.SIG_IGN)
+time.sleep(120)  # stands for a barrier the failed rank never reaches
+"""
+
+
+def _launch(tmp_path, world, fail_rank, ignore_term=False, kill_after=20.0):
+    import importlib.util
+    import time
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    script = tmp_path / "rank.py"
+    script.write_text(RANK_SCRIPT)
+    os.environ["FAIL_RANK"] = str(fail_rank)
+    if ignore_term:
+        os.environ["IGNORE_TERM"] = "1"
+    try:
+        t0 = time.monotonic()
+        rc = bench.launch_ranks(world, cmd=[sys.executable, str(script), str(tmp_path)],
+                                kill_after=kill_after)
+        return rc, time.monotonic() - t0
+    finally:
+        os.environ.pop("FAIL_RANK", None)
+        os.environ.pop("IGNORE_TERM", None)
+
+
+def test_launch_ranks_stops_the_others_and_returns_the_failing_code(tmp_path):
+    """bench.launch_ranks at world 4: every rank gets its RANK / LOCAL_RANK, the
+    same WORLD_SIZE and rendezvous; rank 2 exits 7 while the others wait at a
+    'barrier'; they are stopped and the parent returns 7, not a hang."""
+    import json
+    rc, dt = _launch(tmp_path, 4, fail_rank=2)
+    assert rc == 7 and dt < 30
+    envs = [json.loads((tmp_path / f"rank{r}.json").read_text()) for r in range(4)]
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert {e["WORLD_SIZE"] for e in envs} == {"4"}
+    assert {e["MASTER_ADDR"] for e in envs} == {"127.0.0.1"}
+    assert len({e["MASTER_PORT"] for e in envs}) == 1
+
+
+def test_launch_ranks_kills_ranks_that_ignore_sigterm(tmp_path):
+    rc, dt = _launch(tmp_path, 3, fail_rank=0, ignore_term=True, kill_after=1.0)
+    assert rc == 7 and dt < 30

@@ -1,6 +1,7 @@
 """bench.py's N-rank path end to end on the box's one GPU: two ranks under
-torch.distributed.run with the gloo backend (BDL_BENCH_BACKEND=gloo, ranks
-sharing the device; RCCL needs one GPU per rank).  Checks the contract the
+torch.distributed.run, and two or four ranks started by bench.py itself, with
+the gloo backend (BDL_BENCH_BACKEND=gloo, ranks sharing the device; RCCL
+needs one GPU per rank).  Checks the contract the
 driver relies on at N>1: one JSON line from rank 0, n_gpus = world size,
 value = all ranks' steps / max-over-ranks time, the evaluation collective
 (chains.average_predictive) timed after the timed region."""
@@ -31,38 +32,42 @@ def _free_port():
     return port
 
 
-BENCH_ARGS = ["--gpus", "2", "--steps", "20", "--warmup", "5", "--backbone", "resnet101",
+BENCH_ARGS = ["--steps", "20", "--warmup", "5", "--backbone", "resnet101",
               "--no-autotune", "--e2e-steps", "0", "--no-placement"]
 
 
-@pytest.mark.parametrize("launcher", ["torchrun", "self"])
-def test_bench_two_ranks_gloo(launcher):
-    """Under torch.distributed.run, and as `python bench.py --gpus 2` with no
-    outside launcher (bench.py starts its own ranks): the same one line."""
+@pytest.mark.parametrize("launcher,world", [("torchrun", 2), ("self", 2), ("self", 4)])
+def test_bench_ranks_gloo(launcher, world):
+    """Under torch.distributed.run, and as `python bench.py --gpus N` with no
+    outside launcher (bench.py starts its own ranks): the same one line, with
+    every rank's kernel time and the max-over-ranks wall clock."""
     env = dict(os.environ, BDL_BENCH_BACKEND="gloo")
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     bench = os.path.join(ROOT, "bench.py")
+    args = ["--gpus", str(world)] + BENCH_ARGS
     if launcher == "torchrun":
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", bench] + BENCH_ARGS
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={world}", "--master-addr=127.0.0.1",
+               f"--master-port={_free_port()}", bench] + args
     else:
-        cmd = [sys.executable, bench] + BENCH_ARGS
+        cmd = [sys.executable, bench] + args
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, (p.stdout + p.stderr)[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["steps"] == 20 and d["warmup"] == 5
+    assert d["n_gpus"] == world and d["steps"] == 20 and d["warmup"] == 5
     assert d["scaling"] == "weak" and d["higher_is_better"] is True
-    assert d["value"] > 0 and abs(d["value"] - 2 * 20 / (d["ms_per_step"] * 20 / 1e3)) < 0.02 * d["value"]
-    assert d["config"]["parallelism"].startswith("2 independent chains")
+    assert d["value"] > 0 and \
+        abs(d["value"] - world * 20 / (d["ms_per_step"] * 20 / 1e3)) < 0.02 * d["value"]
+    assert d["config"]["parallelism"].startswith(f"{world} independent chains")
     ec = d["eval_collective"]
     assert ec["backend"] == "gloo" and ec["finite"] is True
     assert "cpu_baseline" not in d  # rank 0 at N=1 only
     assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
     pr = d["per_rank"]  # every rank's own dominant-kernel time
-    assert [r["rank"] for r in pr] == [0, 1]
+    assert [r["rank"] for r in pr] == list(range(world))
     assert all(r["kernel"] == d["roofline"]["kernel"] and r["avg_ms"] > 0 and 0 < r["frac"] < 1
                for r in pr)
 

@@ -43,6 +43,17 @@ def _loader():
     return [(x[i:i + 16], y[i:i + 16]) for i in range(0, 103, 16)]  # 7 batches, last of 7
 
 
+def _shuffled_loader(r):
+    """The reference's training loader shape (datasets.py:45-46: shuffle=True),
+    with a RANK-DEPENDENT shuffle, as chains seeded per rank would draw it."""
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(103, 20, generator=g)
+    y = torch.randint(0, 5, (103,), generator=g)
+    return torch.utils.data.DataLoader(torch.utils.data.TensorDataset(x, y), batch_size=16,
+                                       shuffle=True,
+                                       generator=torch.Generator().manual_seed(1000 + r))
+
+
 def _likelihoods(r):
     # rank-dependent cycle likelihoods (chain r has r + 1 cycles)
     return {c: np.array([0.2 + 0.1 * r + 0.05 * c, 0.3 + 0.02 * c]) for c in range(1, r + 2)}
@@ -58,7 +69,8 @@ def _worker(r, world, port, q):
         net, crit = _net(), nn.CrossEntropyLoss()
         with torch.no_grad():
             acc, nb = R.loss_sums(net, _loader(), crit, "cpu", shard=(r, world))
-        t = torch.tensor([float(acc), float(nb)], dtype=torch.float64)
+            acc2, nb2 = R.loss_sums(net, _shuffled_loader(r), crit, "cpu", shard=(r, world))
+        t = torch.tensor([float(acc), float(nb), float(acc2), float(nb2)], dtype=torch.float64)
         dist.all_reduce(t)
         within, chain_w, joint = chains.chain_gmm_weights(_likelihoods(r))
         g = torch.Generator().manual_seed(50 + r)
@@ -97,10 +109,16 @@ def test_sharded_loss_sums_and_gmm_weights_over_chains(world):
     with torch.no_grad():
         acc, n1 = R.loss_sums(net, _loader(), crit, "cpu")
     assert float(acc) == ref and n1 == nb == 103  # same float64 ops, same order
+    # per-sample losses, for the shuffled loaders whose batches differ by rank
+    with torch.no_grad():
+        x = torch.cat([b[0] for b in _loader()])
+        y = torch.cat([b[1] for b in _loader()])
+        per_sample = nn.CrossEntropyLoss(reduction="sum")(net(x).double(), y).item()
     for r in range(world):
-        tot, cnt = res[r][0]
-        assert cnt == 103
+        tot, cnt, tot2, cnt2 = res[r][0]
+        assert cnt == 103 and cnt2 == 103  # every sample scored exactly once
         np.testing.assert_allclose(tot, ref, rtol=1e-12)
+        np.testing.assert_allclose(tot2, per_sample, rtol=1e-6)  # fp32 batch means
 
     # joint GMM weights over every chain's cycles
     raw = {(r, c): 1.0 / np.mean(1.0 / lk) for r in range(world)
@@ -135,3 +153,21 @@ def test_single_chain_gmm_weights_match_the_reference_formula():
     for c in lik:
         assert within[c] == pytest.approx(ref[c], rel=1e-12)
         assert joint[(0, c)] == pytest.approx(ref[c], rel=1e-12)
+
+
+def test_shard_loader_partitions_samples_and_refuses_what_it_cannot_split():
+    from bayesdll_amd._runner import shard_loader
+    dl = _shuffled_loader(0)
+    seen = []
+    for r in range(3):
+        for x, _ in shard_loader(dl, r, 3):
+            seen.extend(x[:, 0].tolist())
+    allx = torch.cat([b[0] for b in _loader()])[:, 0].tolist()
+    assert sorted(seen) == sorted(allx)
+    assert shard_loader(dl, 0, 1) is dl
+    assert len(shard_loader(_loader(), 1, 3)) == 2  # batches 1, 4 of 7
+    ds = dl.dataset
+    with pytest.raises(ValueError, match="drop_last"):
+        shard_loader(torch.utils.data.DataLoader(ds, batch_size=16, drop_last=True), 0, 2)
+    with pytest.raises(ValueError, match="DataLoader or a list"):
+        shard_loader(iter(_loader()), 0, 2)
