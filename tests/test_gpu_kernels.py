@@ -716,7 +716,7 @@ def test_chunk_mapping_lifetime():
 def test_composites_mapped_one_after_another_do_not_alias():
     """Placement maps and drops many composites of the same chunks.  A freed
     virtual range handed out again was translated to the previous mapping's
-    chunks on this stack (tools/vmm_alias_check.py), so bdl_vmm_unmap keeps
+    chunks on this stack (tools/vmm_alias_repro.cpp), so bdl_vmm_unmap keeps
     ranges reserved: every composite must write exactly its own chunks and
     get a range no earlier mapping had."""
     import random
