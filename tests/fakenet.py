@@ -63,7 +63,7 @@ class FakeNet(nn.Module):
     """nn.Module whose named_parameters() follow `segments` in order."""
 
     def __init__(self, segments=TOY_SEGMENTS, readout_name=TOY_READOUT, grad_seed=1234,
-                 grad_scale=0.5, init=None):
+                 grad_scale=0.5, init=None, grad_table=None):
         super().__init__()
         self.readout_name = readout_name
         self._segments = list(segments)
@@ -77,6 +77,8 @@ class FakeNet(nn.Module):
             mod.register_parameter(parts[-1], nn.Parameter(torch.zeros(shape, dtype=torch.float32)))
         self.grad_seed = grad_seed
         self.grad_scale = grad_scale
+        # optional precomputed grads_for_step vectors (index = step), e.g. on the device
+        self.grad_table = grad_table
         self.step = 0
         if init is not None:
             self.load_flat(init)
@@ -94,9 +96,12 @@ class FakeNet(nn.Module):
     def forward(self, x):
         params = list(self.parameters())
         if torch.is_grad_enabled():
-            g = grads_for_step(self.grad_seed, self.step, self.n, self.grad_scale)
+            if self.grad_table is not None:
+                gt = self.grad_table[self.step].to(params[0].device)
+            else:
+                g = grads_for_step(self.grad_seed, self.step, self.n, self.grad_scale)
+                gt = torch.from_numpy(g).to(params[0].device)
             self.step += 1
-            gt = torch.from_numpy(g).to(params[0].device)
             grads, off = [], 0
             for p in params:
                 k = p.numel()
