@@ -61,15 +61,15 @@ def main(tag, dest=None, backbone="vit_l_32"):
         for r in rows:
             by.setdefault(r["Kernel_Name"], []).append(
                 (int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
-        last = {}
-        for nm, v in by.items():
+        for v in by.values():
             v.sort()
-            last[nm] = v[-1][0]
-        # the kernel dispatched most in the trace's final stretch = the timed loop's
+        # the timed loop's dominant kernel = the step kernel dispatched most
+        # (bench.py times the collect-init kind after its timed region, so the
+        # LAST step dispatch is not the timed loop's)
         step_kernels = {nm: v for nm, v in by.items() if "bdl_step_kernel" in nm or
                         "bdl_adam_kernel" in nm}
         if step_kernels:
-            nm = max(step_kernels, key=lambda k: last[k])
+            nm = max(step_kernels, key=lambda k: len(step_kernels[k]))
             durs = [d for _, d in step_kernels[nm]][-timed:]
             json.dump({"kernel": nm, "timed_launches": len(durs),
                        "avg_ns": round(sum(durs) / len(durs), 1),
