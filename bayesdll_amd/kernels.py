@@ -299,7 +299,7 @@ _TUNED = {}
 ADAM_EXTRA = ("adam_m", "adam_v", "sgd_buf")  # adam_sghmc.Model.extra_vectors
 
 
-def _scratch_launcher(n, dev, method):
+def _scratch_launcher(n, dev, method, placed=True):
     """A closure launching `method`'s production kernel over scratch buffers of
     n elements (the buffers live as long as the closure).  Large scratch
     vectors are placed like a chain's own (flat.placed_vectors): on plain
@@ -312,7 +312,8 @@ def _scratch_launcher(n, dev, method):
     # (bayesdll_amd.placement pool: one search per process and size)
     st = FlatState.from_segments([("w", (int(n),))], None, device=dev,
                                  need_prior=method != "csghmc",
-                                 placement=method if int(n) >= PLACEMENT_MIN_ELEMS else None,
+                                 placement=method if placed and int(n) >= PLACEMENT_MIN_ELEMS
+                                 else None,
                                  extra=ADAM_EXTRA if method == "adam" else ())
     st.theta.zero_()
     if method == "csghmc":
@@ -347,7 +348,7 @@ def _device(device):
         "cuda", torch.cuda.current_device())
 
 
-def autotune(n, device=None, reps=6, candidates=None, method="csghmc"):
+def autotune(n, device=None, reps=6, candidates=None, method="csghmc", placed=True):
     """Pick the fastest launch geometry for an n-element sweep on this device.
 
     The update of every element is independent of the launch geometry (noise
@@ -360,7 +361,7 @@ def autotune(n, device=None, reps=6, candidates=None, method="csghmc"):
     dev = _device(device)
     if candidates is None:
         candidates = AUTOTUNE_CANDIDATES
-    launch = _scratch_launcher(n, dev, method)
+    launch = _scratch_launcher(n, dev, method, placed)
 
     def measure(cfgs, k):
         out = {}
@@ -414,14 +415,14 @@ def prewarm(n, device=None, method="csghmc", seconds=2.5):
     return k
 
 
-def autotune_once(n, device, method):
+def autotune_once(n, device, method, placed=True):
     """autotune() once per (n, device, method) in this process; later calls
     only re-install the cached winner.  BDL_AUTOTUNE=0 keeps the defaults."""
     if os.environ.get("BDL_AUTOTUNE", "1") == "0":
         return None
     key = (int(n), str(device), method)
     if key not in _TUNED:
-        _TUNED[key] = autotune(n, device, method=method)[0]
+        _TUNED[key] = autotune(n, device, method=method, placed=placed)[0]
     else:
         set_launch_config(*_TUNED[key])
     return _TUNED[key]

@@ -253,8 +253,9 @@ class _StackedSampler:
         self.K = K_
         # launch geometry tuned for the stacked size (speed only)
         if st_big(self.state):
+            # (scratch on plain allocations, as the stacked state's own vectors)
             self.state.launch_cfg = K.autotune_once(self.state.n, self.state.device,
-                                                    self.tune_method)
+                                                    self.tune_method, placed=False)
         self.criterion = criterion or torch.nn.CrossEntropyLoss()
         self.step_count = 0
         self.draws = 0

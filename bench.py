@@ -376,7 +376,9 @@ def main():
     elif not a.no_autotune:
         # untimed setup (like cudnn.benchmark): pick the launch geometry for
         # this device; results are identical under every geometry
-        best, tuned = K.autotune(n_all, device=local, method=tune_method)
+        # (its scratch vectors placed like the chain's: their parked set becomes
+        # the chain's, bayesdll_amd.placement)
+        best, tuned = K.autotune(n_all, device=local, method=tune_method, placed=a.placement)
         launch = {"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
                   "autotuned": True,
                   "candidates_ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4) for c, t in tuned.items()},
