@@ -45,7 +45,7 @@ class PosteriorDraw:
         self.count = 0
         self.noise = None if noise_mode == "philox" else torch.empty_like(self.theta)
         self.provider = provider
-        self.placement = None  # draw_buffer's timings, once a Philox draw placed theta
+        self.placement = None  # draw_buffer's info ({} when it placed nothing), once a Philox draw placed theta
         if noise_mode == "external" and provider is None:
             raise RuntimeError("noise_mode='external' needs Model.noise_provider")
 
@@ -59,8 +59,8 @@ class PosteriorDraw:
         def launch(buf):
             K.posterior_sample(buf, mean, m2, var_mode=var_mode, ratio=ratio, seed=self.seed,
                                chain=self.chain, step=step)
-        buf, ms = draw_buffer(self.theta, launch)
-        self.placement = ms or []
+        buf, info = draw_buffer(self.theta, launch)
+        self.placement = info or {}
         if buf is not self.theta:
             self.theta = bind_parameters(self.net, buf)
 

@@ -640,18 +640,44 @@ DRAW_CANDIDATES = 3  # output buffers timed for the posterior-draw sweep
 def draw_buffer(out, launch, candidates=DRAW_CANDIDATES):
     """Pick the posterior-draw output buffer (DESIGN.md §4 placement: the draw
     reads m1 / m2 and writes out, and runs 3-4 % faster with out in the
-    physical class opposite to its reads, which only timing reveals).
-    `launch(buf)` runs the draw into `buf`; `out` and candidates - 1 fresh
-    allocations of its size are each timed (median of 3) and the fastest is
-    returned with the timings; the others go back to torch's cache.  Vectors
-    below PLACEMENT_MIN_ELEMS, or BDL_PLACEMENT=0: `out` unchanged."""
+    physical group opposite to its reads, which only timing reveals).
+    `launch(buf)` runs the draw into `buf` (its inputs' leading buf.numel()
+    elements when buf is shorter than they are).  `out` and candidates - 1
+    fresh allocations of its size are each timed (median of 3); then, with
+    BDL_PLACEMENT=search (the default), a vector built from physical chunks
+    chosen by timing the draw into each (placement.place_one, parked and
+    reused by the next draw copy of this size) competes with the fastest of
+    them.  The winner is returned with
+    {"torch_ms": [...], "chunks": place_one's info or None, "kept": "torch" |
+    "chunks"}; losing allocations go back to torch's cache.  Vectors below
+    PLACEMENT_MIN_ELEMS, or BDL_PLACEMENT=0: (`out`, None)."""
     import os
-    if out.numel() < PLACEMENT_MIN_ELEMS or os.environ.get("BDL_PLACEMENT", "search") == "0":
+    mode = os.environ.get("BDL_PLACEMENT", "search")
+    if out.numel() < PLACEMENT_MIN_ELEMS or mode == "0":
         return out, None
     cands = [out] + [torch.empty_like(out) for _ in range(max(0, candidates - 1))]
     ms = [_time_launch(lambda b=b: launch(b), out.device, 3) for b in cands]
     best = int(np.argmin(ms))
-    return cands[best], [round(t, 4) for t in ms]
+    info = {"torch_ms": [round(t, 4) for t in ms], "chunks": None, "kept": "torch"}
+    if mode != "search":
+        return cands[best], info
+    from . import placement as P
+    free, _ = torch.cuda.mem_get_info(out.device)
+    try:
+        buf, pinfo = P.place_one(out.numel(), out.device, lambda b: (lambda: launch(b)),
+                                 lambda f: _time_launch(f, out.device, 3),
+                                 budget_bytes=int(0.25 * free), pool_key=("draw",),
+                                 beat_ms=ms[best])
+    except RuntimeError as e:  # chunk mappings unavailable: the plain allocations stand
+        import warnings
+        warnings.warn(f"bayesdll_amd: physical-chunk placement unavailable ({e}); "
+                      "the draw keeps torch's allocation")
+        return cands[best], dict(info, chunks={"error": str(e)[:200]})
+    info["chunks"] = pinfo
+    if buf is None:
+        return cands[best], info
+    info["kept"] = "chunks"
+    return buf, info
 
 
 MOMENT_PAIR_ALIGN = 64  # elements: m2 starts 256 B after a 256-B boundary

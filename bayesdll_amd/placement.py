@@ -451,3 +451,96 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
             ps.adopt(nm, m)
     del best_maps
     return keep, info
+
+
+ONE_COMPOSITES = 3  # full-size composites timed by place_one besides allocation order
+
+
+def one_candidates(chunk_ms, per, limit=ONE_COMPOSITES):
+    """Chunk lists for place_one's full-size composites: the `per` fastest
+    chunks of `chunk_ms` (ms per chunk, fastest first), then up to limit - 1
+    further windows of `per` consecutive chunks of that ranking, then the
+    allocation order; no list twice."""
+    ranked = sorted(range(len(chunk_ms)), key=lambda i: chunk_ms[i])
+    cands = []
+    for w in range(limit):
+        ids = ranked[w:w + per]
+        if len(ids) == per and ids not in cands:
+            cands.append(ids)
+    order = list(range(per))
+    if order not in cands:
+        cands.append(order)
+    return cands
+
+
+def place_one(n, device, launcher, time_launch, budget_bytes, spare=None, pool_key=None,
+              beat_ms=None):
+    """One WRITTEN vector (n fp32 elements) from physical chunks, for a sweep
+    whose other streams are fixed (the posterior draw: m1 / m2 given, out
+    chosen; DESIGN.md §4 — it runs fastest with out in the physical group
+    opposite to its reads, which only timing reveals).  `launcher(buf)` returns
+    a zero-argument launch of the sweep writing `buf` (buf.numel() <= n
+    elements: the sweep's inputs are sliced to it); `time_launch(launch)` its
+    median ms.
+
+      1. allocate per + spare chunks (each also mapped alone);
+      2. time the sweep into every chunk (chunk-sized: the reads are the
+         inputs' leading slices);
+      3. map composites of the fastest chunks (the per fastest, then the next
+         ONE_COMPOSITES - 1 windows of the ranking) and the allocation order,
+         and time each at FULL size.
+
+    The fastest composite is returned if it beats `beat_ms` (the caller's best
+    plain allocation), else (None, info): the caller keeps its own buffer.
+    `pool_key`: as for place() — the kept vector is parked when it dies, and
+    the next call with the key takes it back without a search."""
+    import time
+    t_start = time.perf_counter()
+    dev_index = torch.device(device).index
+    if dev_index is None:
+        dev_index = torch.cuda.current_device()
+    key = None if pool_key is None else (dev_index, int(n), ("out",), True, pool_key)
+    got = take_parked(key, n) if key is not None else None
+    if got is not None:
+        vecs, ps = got
+        info = dict(ps.info, reused=True, seconds=round(time.perf_counter() - t_start, 3),
+                    search_seconds=ps.info["seconds"], va_reserved_gb=round(_VA_RESERVED[0] / 2**30, 1))
+        return vecs["out"], info
+    release_pool()
+    per, cb = chunk_geometry(n)
+    k = min(cb // 4, n)  # elements the chunk-sized sweeps write (a 1-chunk vector's chunk is rounded up)
+    spare = (2 * per if spare is None else spare)
+    while spare > 0 and (per + spare) * cb > budget_bytes:
+        spare -= 1
+    if (per + spare) * cb > budget_bytes:
+        return None, {"allocator": "torch", "kept": "torch", "skipped": "over budget"}
+    ch = _Chunks(dev_index, cb)
+    best, best_ms, best_map, comp_ms = None, None, None, []
+    try:
+        ch.add(per + spare)
+        chunk_ms = [time_launch(launcher(v[:k])) for v in ch.views]
+        for ids in one_candidates(chunk_ms, per):
+            m = Mapping(dev_index, [ch.handles[i] for i in ids], cb, n)
+            t = m.tensor()
+            t.zero_()
+            ms = time_launch(launcher(t))
+            comp_ms.append(round(ms, 4))
+            if best_ms is None or ms < best_ms:
+                best, best_ms, best_map, chosen = t, ms, m, ids
+            del t, m
+    finally:
+        ch.release()
+    won = beat_ms is None or best_ms < beat_ms
+    info = {"allocator": "vmm" if won else "torch", "kept": "chunks" if won else "torch",
+            "chunk_mb": cb >> 20, "chunks_per_vector": per, "chunks_allocated": per + spare,
+            "chunk_ms": [round(t, 4) for t in chunk_ms], "composites_ms": comp_ms,
+            "chosen_ms": round(best_ms, 4), "chunks": chosen if won else [],
+            "beat_ms": None if beat_ms is None else round(beat_ms, 4), "reused": False,
+            "seconds": round(time.perf_counter() - t_start, 3),
+            "va_reserved_gb": round(_VA_RESERVED[0] / 2**30, 1)}
+    if not won:
+        return None, info
+    if key is not None:
+        PlacedSet(key, dev_index, info).adopt("out", best_map)
+    del best_map
+    return best, info

@@ -232,12 +232,19 @@ def aux_kernels(st, reps=20):
                      "frac": round(gbs / PEAK_HBM_GBS, 4)}
 
     # the output buffer chosen as the Runners' posterior draws choose it
-    # (flat.draw_buffer: the plain allocation first, then fresh ones, timed)
-    out, cand_ms = draw_buffer(out, lambda b: K.posterior_sample(
+    # (flat.draw_buffer: the plain allocation and fresh ones timed, then a
+    # vector of physical chunks chosen by timing the draw into each competes)
+    out, dinfo = draw_buffer(out, lambda b: K.posterior_sample(
         b, m1, m2, var_mode=L.VAR_WELFORD, ratio=4.0, seed=7, chain=0, step=0))
     timed("posterior_sample", 12, lambda i: K.posterior_sample(
         out, m1, m2, var_mode=L.VAR_WELFORD, ratio=4.0, seed=7, chain=0, step=i))
-    res["posterior_sample"]["out_candidates_ms"] = cand_ms
+    if dinfo is not None:
+        res["posterior_sample"]["out_candidates_ms"] = dinfo["torch_ms"]
+        res["posterior_sample"]["out_kept"] = dinfo["kept"]
+        ci = dinfo["chunks"] or {}
+        res["posterior_sample"]["out_chunks"] = {k: ci.get(k) for k in (
+            "chunk_ms", "composites_ms", "chosen_ms", "reused", "seconds", "error", "skipped")
+            if ci.get(k) is not None}
     res["posterior_sample"]["moments"] = "flat.moment_pair"
     del m1, m2, out
     # the running moments of sgld / sghmc (methods/sgld.py:95-102 seeds them

@@ -85,6 +85,24 @@ def test_draw_buffer_keeps_small_vectors_and_honours_placement_off(monkeypatch):
     assert out is big and ms is None
 
 
+def test_one_candidates_rank_chunks_fastest_first_then_allocation_order():
+    """placement.one_candidates (the posterior draw's output, placement.place_one):
+    the per fastest chunks first, then the next windows of the ranking, then
+    the allocation order; each list once, per distinct chunks in range."""
+    ms = [0.30, 0.10, 0.40, 0.12, 0.11, 0.50]
+    c = P.one_candidates(ms, 2)
+    assert c[0] == [1, 4]                       # the two fastest chunks
+    assert c[1] == [4, 3] and c[2] == [3, 0]    # next windows of the ranking
+    assert c[-1] == [0, 1]                      # allocation order last
+    assert len(c) == P.ONE_COMPOSITES + 1
+    for ids in c:
+        assert len(ids) == 2 and len(set(ids)) == 2 and all(0 <= i < len(ms) for i in ids)
+    # allocation order already among the ranked windows: not repeated
+    assert P.one_candidates([0.1, 0.2, 0.3, 0.4], 2) == [[0, 1], [1, 2], [2, 3]]
+    # one chunk per vector, fewer chunks than windows
+    assert P.one_candidates([0.2, 0.1], 1) == [[1], [0]]
+
+
 
 def test_moment_pair_halves_of_one_allocation(monkeypatch):
     """flat.moment_pair: for vectors of >= PLACEMENT_MIN_ELEMS, m1 / m2 are the
