@@ -6,8 +6,16 @@ cross-chain posterior-predictive average.
 
 Checks:
   * every rank samples its own chain (chain id = rank; eight distinct thetas);
-  * chain 7 of the ensemble is, bit for bit, the chain one process samples
-    alone with chain id 7 (no cross-chain coupling during sampling);
+  * chain 7 of the ensemble is the chain one process samples alone with chain
+    id 7 (no cross-chain coupling during sampling): theta within the north
+    star's 1e-5 relative, and that difference at least 1000x smaller than the
+    one between chains 6 and 7.  Not bit for bit: the fused update is
+    history-independent, but ViT-L/32's autograd is not across processes on
+    this stack — the ensemble's rank 7 (eight processes sharing the GPU) and
+    the lone process land on two fixed low-bit variants of the gradients
+    (theta bit-sums -...466741 and -...447049 on every box since round 2,
+    INTEGRATION.md §6), and which one a process gets depends on its
+    environment, not on the sampler;
   * every rank's predictive is log((1/8) sum_k softmax(s_k)) of the chains' own
     mixture predictives, rebuilt here from each rank's per-chain posterior
     draws (logits_all), and all ranks hold the same one.
@@ -85,10 +93,15 @@ def test_config5_eight_vit_chains_one_gpu(tmp_path):
     assert len({int(r["theta_bits"]) for r in ranks}) == WORLD  # eight distinct chains
 
     last = ranks[WORLD - 1]
-    assert int(single["theta_bits"]) == int(last["theta_bits"])
-    assert single["theta_sum"] == last["theta_sum"]
-    np.testing.assert_array_equal(single["theta_sub"], last["theta_sub"])
-    np.testing.assert_array_equal(single["logits_all"], last["logits_all"])
+    np.testing.assert_allclose(single["theta_sub"], last["theta_sub"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(single["theta_sum"], last["theta_sum"], rtol=1e-5)
+    np.testing.assert_allclose(single["logits_all"], last["logits_all"], rtol=1e-5, atol=1e-5)
+    same = np.abs(single["theta_sub"].astype(np.float64) - last["theta_sub"]).max()
+    other = np.abs(ranks[WORLD - 2]["theta_sub"].astype(np.float64) - last["theta_sub"]).max()
+    assert other > 0 and same * 1000 < other, (same, other)
+    print(f"chain 7 alone vs in the ensemble: max |d theta| {same:.3g} "
+          f"(bit-sums {int(single['theta_bits'])} / {int(last['theta_bits'])}); "
+          f"chain 6 vs 7: {other:.3g}")
 
     # each chain's own mixture predictive from its draws: one cycle, nst draws
     def chain_pred(r):
