@@ -293,6 +293,16 @@ def _use_geometry(state):
 # of every method (cSGHMC; SGLD / SGHMC / Adam with noise) exist at unroll
 # depths 1, 2 and 4.
 AUTOTUNE_CANDIDATES = ((2, 1, 1), (1, 4, 1), (3, 1, 1), (2, 4, 1), (1, 2, 1), (2, 2, 1))
+# per sampler family, the geometries that won somewhere in the interleaved
+# 13-geometry probe on a placed ViT-L/32 state (tools/geom_methods.py,
+# profiles/round3/aux/geom_methods.jsonl): SGLD 3 x 4 by 0.5 % over 2 x 4;
+# Adam-SGHMC 1 x 1 by 1.5 % and 4 x 4 by 0.3 % over 2 x 4 (seven streams: fewer
+# accesses in flight per CU pay); cSGHMC 1 x 4 by >= 1.9 % over every other
+AUTOTUNE_BY_METHOD = {
+    "csghmc": AUTOTUNE_CANDIDATES,
+    "sgld": AUTOTUNE_CANDIDATES + ((3, 4, 1), (4, 4, 1)),
+    "adam": AUTOTUNE_CANDIDATES + ((1, 1, 1), (4, 4, 1)),
+}
 _TUNED = {}
 
 
@@ -360,7 +370,7 @@ def autotune(n, device=None, reps=6, candidates=None, method="csghmc", placed=Tr
     import numpy as np
     dev = _device(device)
     if candidates is None:
-        candidates = AUTOTUNE_CANDIDATES
+        candidates = AUTOTUNE_BY_METHOD.get(method, AUTOTUNE_CANDIDATES)
     launch = _scratch_launcher(n, dev, method, placed)
 
     def measure(cfgs, k):
