@@ -1,5 +1,6 @@
 """bench.py's N-rank path end to end on the box's one GPU: two ranks under
-torch.distributed.run, and two or four ranks started by bench.py itself, with
+torch.distributed.run (two, and eight as the driver's N=8 run), and two or
+four ranks started by bench.py itself, with
 the gloo backend (BDL_BENCH_BACKEND=gloo, ranks sharing the device; RCCL
 needs one GPU per rank).  Checks the contract the
 driver relies on at N>1: one JSON line from rank 0, n_gpus = world size,
@@ -36,7 +37,10 @@ BENCH_ARGS = ["--steps", "20", "--warmup", "5", "--backbone", "resnet101",
               "--no-autotune", "--e2e-steps", "0", "--no-placement"]
 
 
-@pytest.mark.parametrize("launcher,world", [("torchrun", 2), ("self", 2), ("self", 4)])
+# ("torchrun", 8): the driver's own N=8 command shape (torch.distributed.run
+# --nproc-per-node 8), eight ranks sharing the one GPU
+@pytest.mark.parametrize("launcher,world", [("torchrun", 2), ("self", 2), ("self", 4),
+                                            ("torchrun", 8)])
 def test_bench_ranks_gloo(launcher, world):
     """Under torch.distributed.run, and as `python bench.py --gpus N` with no
     outside launcher (bench.py starts its own ranks): the same one line, with
