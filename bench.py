@@ -69,9 +69,11 @@ def parse():
                     help="untimed back-to-back launches before the measurement (clock ramp)")
     ap.add_argument("--no-placement", dest="placement", action="store_false",
                     help="allocate the chain vectors without placement tuning")
-    ap.add_argument("--event-stride", type=int, default=5,
+    ap.add_argument("--event-stride", type=int, default=0,
                     help="bracket every k-th timed launch (and the first of each kind) with "
-                         "HIP events; 1 = all.  Each bracket costs the stream ~5 us (two event "
+                         "HIP events; 1 = all, 0 (default) = max(1, min(5, steps // 10)), i.e. "
+                         "2 at the driver's 20 steps, 5 at 200.  Each bracket costs the stream "
+                         "~5 us (two event "
                          "packets between kernels): at 1 the line's ms_per_step read 1.0239-1.0248 "
                          "vs 1.0186-1.0191 at 10 on one box, the kernel averages unchanged")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -534,7 +536,7 @@ def main():
     for k in range(a.warmup):
         step(k)
     torch.cuda.synchronize()
-    timer = LaunchTimer(a.event_stride)
+    timer = LaunchTimer(a.event_stride or max(1, min(5, a.steps // 10)))
     kinds = []
     if dist is not None:
         dist.barrier()
