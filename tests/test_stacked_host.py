@@ -173,7 +173,11 @@ def _stacked_worker(r, world, port, q):
         torch.manual_seed(0)
         S = stacked.StackedCSGHMC(Net(), 2, _args(), init="reinit", seed=10 + 2 * r)
         x = torch.randn(6, 13, generator=torch.Generator().manual_seed(5))
-        q.put((r, S.chain0, S.chain_logits(x), S.predictive_logprob(x)))
+        # numpy copies, not tensors: a tensor put on a torch.multiprocessing queue
+        # travels as a shared-memory handle that the receiver can only open while
+        # this process is alive, and it exits right after (a flaky receive)
+        q.put((r, S.chain0, S.chain_logits(x).detach().numpy().copy(),
+               S.predictive_logprob(x).detach().numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -193,8 +197,8 @@ def test_stacked_predictive_averages_over_processes():
         p.start()
     res = {}
     for _ in range(2):
-        r, c0, logits, lp = q.get(timeout=120)
-        res[r] = (c0, logits, lp)
+        r, c0, logits, lp = q.get(timeout=300)
+        res[r] = (c0, torch.from_numpy(logits), torch.from_numpy(lp))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
