@@ -169,6 +169,9 @@ class FusedModelBase(nn.Module):
             if steps_timed > 0:  # sampled update timing, logged once per epoch
                 self._state.timer = K.StepTimer(steps_timed)
             self._state.launch_cfg = launch_cfg
+            if launch_cfg is not None:
+                self._state.collect_cfg = K.collect_config(n_all, params[0].device,
+                                                           self.tune_method)
         return self._state
 
     @property

@@ -145,7 +145,10 @@ class StepTimer:
 
 
 def _launch(state, fn, a, adam=None):
-    _use_geometry(state)
+    # the steady-state collect kinds (m1 / m2 read and written) have their own
+    # geometry; the cycle's first collect (m1 / m2 only written) runs at the
+    # step's: 1.42 ms there vs 1.48 at the Welford collect's 1 x 1
+    _use_geometry(state, a.collect in (L.COLLECT_WELFORD, L.COLLECT_MEAN))
     t = getattr(state, "timer", None)
     e0 = t.begin() if t is not None else None
     fn()
@@ -277,12 +280,15 @@ def restore_launch_config(packed):
     return set_launch_config((packed >> 8) & 0xFFFF, packed & 0xFF, (packed >> 24) & 0xFF)
 
 
-def _use_geometry(state):
+def _use_geometry(state, collect=False):
     """Install the geometry tuned for this state's size (state.launch_cfg, set
-    from autotune_once) if another state's is active: the library's launch
+    from autotune_once; state.collect_cfg for the steps that also read and
+    update the posterior moments, when tuned) if another is active: the library's launch
     configuration is process-wide, and a process may hold states of very
     different sizes (e.g. a one-chain sampler and a stacked one)."""
-    cfg = getattr(state, "launch_cfg", None)
+    cfg = getattr(state, "collect_cfg", None) if collect else None
+    if cfg is None:
+        cfg = getattr(state, "launch_cfg", None)
     if cfg is not None and cfg != _ACTIVE[0]:
         set_launch_config(*cfg)
 
@@ -304,6 +310,14 @@ AUTOTUNE_BY_METHOD = {
     "adam": AUTOTUNE_CANDIDATES + ((1, 1, 1), (4, 4, 1)),
 }
 _TUNED = {}
+_TUNED_COLLECT = {}
+# the collect steps (the step plus the posterior-moment update: cSGHMC Welford
+# m1 / M2, SGLD / Adam running m1 / m2 — four to six more streams) are tuned
+# separately over the method's candidates plus 1 x 1: the cSGHMC Welford
+# collect ran 1.778 ms at 1 x 1 vs 1.800 at the explore's 1 x 4 and >= 1.83 at
+# every other geometry (tools/geom_methods.py METHODS=collect,
+# profiles/round3/aux/geom_collect.jsonl; round 1's sweep: 1 x 1 best too)
+COLLECT_EXTRA = ((1, 1, 1),)
 
 
 ADAM_EXTRA = ("adam_m", "adam_v", "sgd_buf")  # adam_sghmc.Model.extra_vectors
@@ -311,12 +325,21 @@ ADAM_EXTRA = ("adam_m", "adam_v", "sgd_buf")  # adam_sghmc.Model.extra_vectors
 
 def _scratch_launcher(n, dev, method, placed=True):
     """A closure launching `method`'s production kernel over scratch buffers of
-    n elements (the buffers live as long as the closure).  Large scratch
-    vectors are placed like a chain's own (flat.placed_vectors): on plain
-    allocations that happen to pair slowly, geometries rank differently than
-    on the placed vectors the sampler then sweeps (3 of 38 round-2 bench runs
-    kept a geometry 1.5-3 % slower there than 1 x 4)."""
-    from .flat import PLACEMENT_MIN_ELEMS, FlatState
+    n elements (the buffers live as long as the closure)."""
+    return _scratch_launchers(n, dev, method, placed)[0]
+
+
+def _scratch_launchers(n, dev, method, placed=True):
+    """Closures launching `method`'s production kernel over scratch buffers of
+    n elements — (plain step, collect step: the same with the posterior-moment
+    update; its m1 / m2 are allocated at its first call, for cSGHMC as the
+    Runner allocates a cycle's Welford pair) — the buffers live as long as the
+    closures.  Large scratch vectors are placed like a chain's own
+    (flat.placed_vectors): on plain allocations that happen to pair slowly,
+    geometries rank differently than on the placed vectors the sampler then
+    sweeps (3 of 38 round-2 bench runs kept a geometry 1.5-3 % slower there
+    than 1 x 4)."""
+    from .flat import PLACEMENT_MIN_ELEMS, FlatState, moment_pair
     # the same roles as the sampler's own state, so that its placed set, parked
     # when this scratch state dies, is the one the sampler's state then takes
     # (bayesdll_amd.placement pool: one search per process and size)
@@ -350,7 +373,25 @@ def _scratch_launcher(n, dev, method, placed=True):
             adam_step(st, L.ADAM_SGHMC, **kw)
     else:
         raise ValueError(f"unknown method {method!r}")
-    return launch
+    moms = []
+
+    def launch_collect():
+        if not moms:
+            moms.extend(moment_pair(int(n), dev) if method == "csghmc" else
+                        (torch.zeros_like(st.theta), torch.zeros_like(st.theta)))
+            moms[0].copy_(st.theta)
+            moms[1].zero_()
+        if method == "csghmc":
+            sgmcmc_step(st, L.CSGHMC, lrs=(1e-4, 1e-4), noise_scale=(1e-7, 1e-7),
+                        noise_mode=L.NOISE_PHILOX, one_minus_alpha=0.9, prior_sig=1.0,
+                        collect=L.COLLECT_WELFORD, mom1=moms[0], mom2=moms[1], collect_a=3.0)
+        elif method == "sgld":
+            sgmcmc_step(st, L.SGLD, collect=L.COLLECT_MEAN, mom1=moms[0], mom2=moms[1],
+                        collect_a=2.0, collect_b=3.0, **kw)
+        else:
+            adam_step(st, L.ADAM_SGHMC, collect=L.COLLECT_MEAN, mom1=moms[0], mom2=moms[1],
+                      collect_a=2.0, collect_b=3.0, **kw)
+    return launch, launch_collect
 
 
 def _device(device):
@@ -358,7 +399,8 @@ def _device(device):
         "cuda", torch.cuda.current_device())
 
 
-def autotune(n, device=None, reps=6, candidates=None, method="csghmc", placed=True):
+def autotune(n, device=None, reps=6, candidates=None, method="csghmc", placed=True,
+             collect=False):
     """Pick the fastest launch geometry for an n-element sweep on this device.
 
     The update of every element is independent of the launch geometry (noise
@@ -366,43 +408,53 @@ def autotune(n, device=None, reps=6, candidates=None, method="csghmc", placed=Tr
     results.  Times the method's production kernel (cSGHMC exploration; SGLD
     + SGD momentum with Philox noise; Adam-SGHMC + SGD momentum) on scratch
     buffers (freed afterwards) and installs the winner process-wide.  Returns
-    (config, {config: ms})."""
+    (config, {config: ms}); with collect=True, (config, {config: ms},
+    collect config, {config: ms}) — the collect step tuned on the same
+    scratch state over the candidates plus COLLECT_EXTRA (not installed)."""
     import numpy as np
     dev = _device(device)
     if candidates is None:
         candidates = AUTOTUNE_BY_METHOD.get(method, AUTOTUNE_CANDIDATES)
-    launch = _scratch_launcher(n, dev, method, placed)
+    launch, launch_collect = _scratch_launchers(n, dev, method, placed)
 
-    def measure(cfgs, k):
+    def pick(fn, cands):
+        # round 1: every candidate; round 2: the three fastest again with twice
+        # the repetitions, averaged with round 1 (damps the +-1-2 % burst-to-burst noise)
+        times = measure(fn, cands, reps)
+        top = sorted(times, key=times.get)[:3]
+        again = measure(fn, top, 2 * reps)
+        for cfg in top:
+            times[cfg] = 0.5 * (times[cfg] + again[cfg])
+        return min(top, key=times.get), times
+
+    def measure(fn, cfgs, k):
         out = {}
         for cfg in cfgs:
             set_launch_config(*cfg)
             for _ in range(2):
-                launch()
+                fn()
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(k)]
             for e0, e1 in ev:
                 e0.record()
-                launch()
+                fn()
                 e1.record()
             torch.cuda.synchronize(dev)
             out[cfg] = float(np.median([a.elapsed_time(b) for a, b in ev]))
         return out
 
-    # round 1: every candidate; round 2: the three fastest again with twice the
-    # repetitions, averaged with round 1 (damps the +-1-2 % burst-to-burst noise)
-    times = measure(candidates, reps)
-    top = sorted(times, key=times.get)[:3]
-    again = measure(top, 2 * reps)
-    for cfg in top:
-        times[cfg] = 0.5 * (times[cfg] + again[cfg])
-    best = min(top, key=times.get)
+    best, times = pick(launch, candidates)
+    res = (best, times)
+    if collect:
+        cbest, ctimes = pick(launch_collect, tuple(candidates) + tuple(
+            c for c in COLLECT_EXTRA if c not in candidates))
+        res = (best, times, cbest, ctimes)
     set_launch_config(*best)
-    del launch
+    del launch, launch_collect
     import gc
     gc.collect()  # the scratch state now, so that its placed set is parked for the chain
     torch.cuda.empty_cache()
-    return best, times
+    return res
 
 
 def prewarm(n, device=None, method="csghmc", seconds=2.5):
@@ -426,13 +478,22 @@ def prewarm(n, device=None, method="csghmc", seconds=2.5):
 
 
 def autotune_once(n, device, method, placed=True):
-    """autotune() once per (n, device, method) in this process; later calls
-    only re-install the cached winner.  BDL_AUTOTUNE=0 keeps the defaults."""
+    """autotune() (plain and collect steps) once per (n, device, method) in this
+    process; later calls only re-install the cached winner.  Returns the plain
+    step's geometry (collect_config: the collect step's).  BDL_AUTOTUNE=0
+    keeps the defaults."""
     if os.environ.get("BDL_AUTOTUNE", "1") == "0":
         return None
     key = (int(n), str(device), method)
     if key not in _TUNED:
-        _TUNED[key] = autotune(n, device, method=method, placed=placed)[0]
+        best, _, cbest, _ = autotune(n, device, method=method, placed=placed, collect=True)
+        _TUNED[key], _TUNED_COLLECT[key] = best, cbest
     else:
         set_launch_config(*_TUNED[key])
     return _TUNED[key]
+
+
+def collect_config(n, device, method):
+    """The collect step's geometry autotune_once found for (n, device, method),
+    or None (not tuned: the plain step's geometry is used)."""
+    return _TUNED_COLLECT.get((int(n), str(device), method))

@@ -390,11 +390,16 @@ def main():
         # this device; results are identical under every geometry
         # (its scratch vectors placed like the chain's: their parked set becomes
         # the chain's, bayesdll_amd.placement)
-        best, tuned = K.autotune(n_all, device=local, method=tune_method, placed=a.placement)
+        best, tuned, cbest, ctuned = K.autotune(n_all, device=local, method=tune_method,
+                                                placed=a.placement, collect=True)
         launch = {"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
                   "autotuned": True,
                   "candidates_ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4) for c, t in tuned.items()},
-                  "tuned_on": a.method}
+                  "tuned_on": a.method,
+                  # the collect steps' own geometry (kernels._use_geometry)
+                  "collect": {"blocks_per_cu": cbest[0], "unroll": cbest[1],
+                              "candidates_ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4)
+                                                for c, t in ctuned.items()}}}
     else:
         launch = {"default": True, "autotuned": False}
     dev = torch.device("cuda", local)
@@ -403,6 +408,8 @@ def main():
     st = FlatState.from_segments(segs, readout, device=dev, need_prior=sgld,
                                  placement=tune_method if a.placement else None,
                                  extra=("adam_m", "adam_v", "sgd_buf") if adam else ())
+    if launch.get("autotuned"):
+        st.launch_cfg, st.collect_cfg = best, cbest
     gen = torch.Generator(device=dev).manual_seed(42 + rank)
     if sgld:  # config 3: theta0 ~ N(0, 0.02^2) (pretrained stand-in), theta = theta0 + N(0, 1e-3^2)
         st.prior.normal_(0.0, 0.02, generator=gen)

@@ -38,14 +38,37 @@ def time_geom(launch, cfg, reps):
     return float(np.median([a.elapsed_time(b) for a, b in ev]))
 
 
+def collect_launcher(n):
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd.flat import FlatState, moment_pair
+    st = FlatState.from_segments([("w", (int(n),))], None, device="cuda", placement="csghmc")
+    st.theta.normal_(0, 0.02)
+    st.grad.normal_(0, 1e-3)
+    m1, m2 = moment_pair(n, st.device)
+    m1.copy_(st.theta)
+    m2.zero_()
+
+    def launch():
+        K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-4, 1e-2), noise_scale=(1e-7, 1e-6),
+                      noise_mode=L.NOISE_PHILOX, one_minus_alpha=0.82, prior_sig=1.0,
+                      collect=L.COLLECT_WELFORD, mom1=m1, mom2=m2, collect_a=3.0, seed=42,
+                      chain=0, step=1)
+    return launch
+
+
 def main():
     reps = int(os.environ.get("REPS", "10"))
     rounds = int(os.environ.get("ROUNDS", "3"))
     methods = os.environ.get("METHODS", "csghmc,sgld,adam").split(",")
+    # "collect": the cSGHMC Welford collect step (Philox + m1 / m2 of one
+    # flat.moment_pair) on the explore's placed scratch state
     segs, _ = segments("vit_l_32")
     n = sum(int(np.prod(s)) for _, s in segs)
     for method in methods:
-        launch = K._scratch_launcher(n, torch.device("cuda", 0), method, placed=True)
+        if method == "collect":
+            launch = collect_launcher(n)
+        else:
+            launch = K._scratch_launcher(n, torch.device("cuda", 0), method, placed=True)
         per = {g: [] for g in GEOMS}
         for r in range(rounds):
             order = GEOMS if r % 2 == 0 else GEOMS[::-1]
