@@ -317,15 +317,85 @@ def candidate_assignments(times, nchunks, names, per, limit=COMPOSITES):
     return cands
 
 
+# which chunk pairs the search times: "all" ordered pairs (K (K - 1)
+# timings), or "ref" — every chunk as mom against chunk 0 as theta (K - 1
+# timings), the pairing relation being one of physical groups:
+# chunks slow against chunk 0 share its group and go with it, the fastest
+# against it take the other role (BDL_PLACEMENT_PAIRS overrides)
+PAIRS = os.environ.get("BDL_PLACEMENT_PAIRS", "all")
+
+
+def _ref_split(times0, per):
+    """times0 {j: ms of (theta = chunk 0, mom = chunk j)}: (slow, fast) chunk
+    lists — slow: above the midpoint of the fastest and slowest time, slowest
+    first (chunk 0's own group); fast: the rest, fastest first — or None when
+    the times show no two groups (spread under FAST_PAIR) or too few of
+    either (slow >= per - 1, fast >= per)."""
+    if not times0:
+        return None
+    lo, hi = min(times0.values()), max(times0.values())
+    if not lo < FAST_PAIR * hi:
+        return None
+    mid = 0.5 * (lo + hi)
+    slow = sorted((j for j, t in times0.items() if t > mid), key=lambda j: -times0[j])
+    fast = sorted((j for j, t in times0.items() if t <= mid), key=lambda j: times0[j])
+    if len(slow) < per - 1 or len(fast) < per:
+        return None
+    return slow, fast
+
+
+def ref_candidates(times0, nchunks, names, per, limit=COMPOSITES):
+    """Chunk ids per role for the full-size candidates of the "ref" search:
+    the allocation order first, then up to `limit` assignments with theta =
+    chunk 0 plus the per - 1 next-slowest chunks against it (its group) and
+    mom = per chunks of the fast group — windows sliding along both rankings —
+    and the same with theta / mom swapped; the other roles take the remaining
+    chunks in allocation order.  No chunk serves two roles."""
+    it, im = names.index("theta"), names.index("mom")
+
+    def assign(th, mo):
+        used = set(th) | set(mo)
+        rest = [k for k in range(nchunks) if k not in used]
+        out, r = {}, 0
+        for q, nm in enumerate(names):
+            if q == it:
+                out[nm] = list(th)
+            elif q == im:
+                out[nm] = list(mo)
+            else:
+                out[nm] = rest[r * per:(r + 1) * per]
+                r += 1
+        return out
+
+    cands = [{nm: list(range(q * per, (q + 1) * per)) for q, nm in enumerate(names)}]
+    split = _ref_split(times0, per)
+    if split is None:
+        return cands
+    slow, fast = split
+    w = 0
+    while len(cands) <= limit:
+        th = [0] + slow[w:w + per - 1]
+        mo = fast[w:w + per]
+        if len(th) < per or len(mo) < per:
+            break
+        for a, b in ((th, mo), (mo, th)):
+            c = assign(a, b)
+            if len(cands) <= limit and c not in cands and \
+                    all(len(v) == per for v in c.values()):
+                cands.append(c)
+        w += 1
+    return cands
+
+
 def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, search=True,
-          with_torch=True, pool_key=None):
+          with_torch=True, pool_key=None, pairs=None):
     """Allocate `names` (fp32, n elements each, zeroed) from physical chunks,
     theta / mom paired fast.  `launcher(roles: {name: tensor}, n)` returns a
     zero-argument launch of the sampler's kernel; `time_launch(launch)` its
     median ms.  search=False: chunks mapped in allocation order, no pair
-    timing.  `pool_key`: the kept vectors form a PlacedSet parked under this
-    key when they die, and a set parked under it is reused instead of a new
-    search.  Returns ({name: tensor}, info)."""
+    timing.  `pairs`: "all" or "ref" (PAIRS).  `pool_key`: the kept vectors
+    form a PlacedSet parked under this key when they die, and a set parked
+    under it is reused instead of a new search.  Returns ({name: tensor}, info)."""
     import time
     t_start = time.perf_counter()
     dev_index = torch.device(device).index
@@ -369,14 +439,18 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
                     r += 1
             return out
 
+        pairs = pairs or PAIRS
+        if pairs not in ("all", "ref"):
+            raise ValueError(f"BDL_PLACEMENT_PAIRS must be all or ref, got {pairs!r}")
         times, rounds = {}, 0
         while search:
-            for i in range(len(ch.views)):
+            for i in range(len(ch.views) if pairs == "all" else 1):
                 for j in range(len(ch.views)):
                     if i != j and (i, j) not in times:
                         times[(i, j)] = time_launch(launcher(roles_for(i, j), nchunk))
-            if _has_fast_pair(times.values()) or rounds >= SPARE_ROUNDS or \
-                    (len(ch.views) + spare) * cb > budget_bytes:
+            done = _has_fast_pair(times.values()) if pairs == "all" else \
+                _ref_split({j: t for (_, j), t in times.items()}, per) is not None
+            if done or rounds >= SPARE_ROUNDS or (len(ch.views) + spare) * cb > budget_bytes:
                 break
             ch.add(spare)
             rounds += 1
@@ -386,7 +460,8 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
                     for nm, ids in assign.items()}
             return maps, {nm: m.tensor() for nm, m in maps.items()}
 
-        cands = candidate_assignments(times, len(ch.views), names, per)
+        cands = candidate_assignments(times, len(ch.views), names, per) if pairs == "all" \
+            else ref_candidates({j: t for (_, j), t in times.items()}, len(ch.views), names, per)
         best, best_ms, comp_ms, best_src, best_maps = None, None, [], None, None
         for c in cands:
             maps, vec = composite(c)
@@ -433,7 +508,7 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
         ch.release()
     pair_ms = sorted(times.values()) or [float("nan")]
     info = {"allocator": "torch" if best_src == "torch" else "vmm", "search": bool(search), "chunk_mb": cb >> 20,
-            "chunks_per_vector": per, "chunks_allocated": nk,
+            "chunks_per_vector": per, "chunks_allocated": nk, "pairs": pairs if search else None,
             "pairs_timed": len(times), "pair_ms_min": round(pair_ms[0], 4),
             "pair_ms_median": round(pair_ms[len(pair_ms) // 2], 4),
             "pair_ms_max": round(pair_ms[-1], 4),

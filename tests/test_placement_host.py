@@ -126,3 +126,43 @@ def test_moment_pair_halves_of_one_allocation(monkeypatch):
     monkeypatch.setenv("BDL_PLACEMENT", "0")
     a, b = F.moment_pair(F.PLACEMENT_MIN_ELEMS, "cpu")
     assert a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr()
+
+
+def test_ref_split_needs_two_groups_and_enough_of_each():
+    """placement._ref_split (the "ref" search): chunks slow against chunk 0 share
+    its group, the rest are the fast group; no split without a spread or
+    without per - 1 slow and per fast chunks."""
+    t = {1: 1.05, 2: 0.96, 3: 1.06, 4: 0.95, 5: 0.97, 6: 1.04, 7: 0.955}
+    slow, fast = P._ref_split(t, 2)
+    assert slow == [3, 1, 6] and fast == [4, 7, 2, 5]
+    assert P._ref_split({1: 1.0, 2: 0.995, 3: 1.001}, 2) is None      # one group
+    assert P._ref_split({1: 0.95, 2: 0.96, 3: 1.05}, 3) is None       # one slow < per - 1
+    assert P._ref_split({1: 1.05, 2: 1.06, 3: 0.95}, 2) is None       # one fast < per
+    assert P._ref_split({}, 1) is None
+
+
+@pytest.mark.parametrize("names", [["theta", "mom"], ["theta", "mom", "prior"],
+                                   ["theta", "mom", "prior", "adam_m", "adam_v", "sgd_buf"]])
+@pytest.mark.parametrize("per", [1, 2, 3])
+def test_ref_candidates_pair_chunk0s_group_with_the_fast_group(names, per):
+    nchunks = len(names) * per + 2 * per
+    rng = random.Random(7 * per + len(names))
+    # chunks 0..per (chunk 0's group) slow against 0, the rest fast, with noise
+    t0 = {j: (1.05 if j <= per else 0.96) + 0.005 * rng.random() for j in range(1, nchunks)}
+    cands = P.ref_candidates(t0, nchunks, names, per)
+    assert cands[0] == {nm: list(range(q * per, (q + 1) * per)) for q, nm in enumerate(names)}
+    assert 2 <= len(cands) <= P.COMPOSITES + 1
+    group0 = set(range(per + 1))
+    for c in cands:
+        ids = [k for nm in names for k in c[nm]]
+        assert all(len(c[nm]) == per for nm in names)
+        assert len(ids) == len(set(ids)) and all(0 <= k < nchunks for k in ids)
+    for c in cands[1:]:
+        th, mo = set(c["theta"]), set(c["mom"])
+        # one of theta / mom is chunk 0's group, the other entirely the fast group
+        assert (th <= group0 and not mo & group0) or (mo <= group0 and not th & group0)
+    # the first: theta = chunk 0 and its group, mom = the fastest chunks
+    fastest = sorted((j for j in t0 if j > per), key=t0.get)[:per]
+    assert cands[1]["theta"][0] == 0 and cands[1]["mom"] == fastest
+    # no split: allocation order only
+    assert P.ref_candidates({j: 1.0 for j in range(1, nchunks)}, nchunks, names, per) == cands[:1]
