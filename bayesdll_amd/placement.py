@@ -415,7 +415,9 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
     nchunk = cb // 4
     nroles = len(names)
     it, im = names.index("theta"), names.index("mom")
-    spare = (2 * per if spare is None else spare) if search else 0
+    if spare is None:
+        spare = int(os.environ.get("BDL_PLACEMENT_SPARE", "0")) or 2 * per
+    spare = spare if search else 0
     # footprint up front: the chunks and the torch competitors are
     # alive together; drop the competition, then the spares, if over budget
     if TORCH_EXTRA < 0 or (nroles * per + spare) * cb + (nroles + TORCH_EXTRA) * 4 * n > budget_bytes:
