@@ -70,7 +70,12 @@ from . import _lib as L
 CHUNK_TARGET = int(os.environ.get("BDL_CHUNK_MB", "1024")) << 20
 ALIGN = 2 << 20          # chunk sizes are multiples of 2 MiB (large-page mappings)
 FAST_PAIR = 0.97         # a pair this much faster than the median pair is worth taking
-SPARE_ROUNDS = 2         # at most this many rounds of extra chunks while none is seen
+# when the first pool shows no fast pair, chunks are added `spare` at a time and
+# each new one is timed against chunk 0 only, until one group is this much
+# faster than chunk 0's own (the best of the three pairing levels, DESIGN.md §4,
+# not the middle one) or the pool holds MAX_CHUNKS / the budget
+FAST_REF = 0.94
+MAX_CHUNKS = int(os.environ.get("BDL_PLACEMENT_MAX_CHUNKS", "64"))
 COMPOSITES = 6           # full-size candidate assignments timed besides allocation order
 # plain torch allocations competing with the chunk composites: TORCH_VECTORS
 # of them (the roles + extras; BDL_PLACEMENT_TORCH overrides), every unordered
@@ -344,6 +349,18 @@ def _ref_split(times0, per):
     return slow, fast
 
 
+def _ref_found(times0, per):
+    """The escalation's stop rule: a split (_ref_split) whose fastest chunk is
+    FAST_REF faster than chunk 0's group (the median of its slow times; the
+    slowest time when the group is chunk 0 alone)."""
+    split = _ref_split(times0, per)
+    if split is None:
+        return False
+    slow, fast = split
+    ref = sorted(times0[j] for j in slow)[len(slow) // 2] if slow else max(times0.values())
+    return times0[fast[0]] < FAST_REF * ref
+
+
 def ref_candidates(times0, nchunks, names, per, limit=COMPOSITES):
     """Chunk ids per role for the full-size candidates of the "ref" search:
     the allocation order first, then up to `limit` assignments with theta =
@@ -445,25 +462,39 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
         if pairs not in ("all", "ref"):
             raise ValueError(f"BDL_PLACEMENT_PAIRS must be all or ref, got {pairs!r}")
         times, rounds = {}, 0
-        while search:
+
+        def times0():
+            return {j: t for (i, j), t in times.items() if i == 0}
+        if search:
+            # the first pool: every ordered pair ("all") or every chunk against chunk 0
             for i in range(len(ch.views) if pairs == "all" else 1):
                 for j in range(len(ch.views)):
-                    if i != j and (i, j) not in times:
+                    if i != j:
                         times[(i, j)] = time_launch(launcher(roles_for(i, j), nchunk))
-            done = _has_fast_pair(times.values()) if pairs == "all" else \
-                _ref_split({j: t for (_, j), t in times.items()}, per) is not None
-            if done or rounds >= SPARE_ROUNDS or (len(ch.views) + spare) * cb > budget_bytes:
-                break
-            ch.add(spare)
-            rounds += 1
+            found = _has_fast_pair(times.values()) if pairs == "all" else _ref_found(times0(), per)
+            # no fast pair yet: the pool's chunks sit in one physical group (on
+            # some boxes a group spans more than 16 chunks of 586 MB: a 16-chunk
+            # all-pairs search kept 1.03-1.04 ms where 28 chunks reached 0.96,
+            # profiles/round3/aux/spare_ab.jsonl) — add chunks and time each new
+            # one against chunk 0 only until another group shows
+            while not found and spare > 0 and len(ch.views) + spare <= MAX_CHUNKS and \
+                    (len(ch.views) + spare) * cb <= budget_bytes:
+                k0 = len(ch.views)
+                ch.add(spare)
+                rounds += 1
+                for j in range(k0, len(ch.views)):
+                    times[(0, j)] = time_launch(launcher(roles_for(0, j), nchunk))
+                found = _ref_found(times0(), per)
 
         def composite(assign):
             maps = {nm: Mapping(dev_index, [ch.handles[k] for k in ids], cb, n)
                     for nm, ids in assign.items()}
             return maps, {nm: m.tensor() for nm, m in maps.items()}
 
-        cands = candidate_assignments(times, len(ch.views), names, per) if pairs == "all" \
-            else ref_candidates({j: t for (_, j), t in times.items()}, len(ch.views), names, per)
+        cands = candidate_assignments(times, len(ch.views), names, per) if pairs == "all" else []
+        for c in ref_candidates(times0(), len(ch.views), names, per):
+            if c not in cands:
+                cands.append(c)
         best, best_ms, comp_ms, best_src, best_maps = None, None, [], None, None
         for c in cands:
             maps, vec = composite(c)
@@ -511,6 +542,8 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
     pair_ms = sorted(times.values()) or [float("nan")]
     info = {"allocator": "torch" if best_src == "torch" else "vmm", "search": bool(search), "chunk_mb": cb >> 20,
             "chunks_per_vector": per, "chunks_allocated": nk, "pairs": pairs if search else None,
+            "escalation_rounds": rounds,
+            "ref_ms": [round(t, 4) for _, t in sorted(times0().items())],
             "pairs_timed": len(times), "pair_ms_min": round(pair_ms[0], 4),
             "pair_ms_median": round(pair_ms[len(pair_ms) // 2], 4),
             "pair_ms_max": round(pair_ms[-1], 4),
