@@ -18,12 +18,16 @@ into one virtual range (hipMemMap), so the pairing is chosen chunk by chunk:
   2. time the method's production kernel on every ordered chunk pair
      (theta = chunk i, momentum = chunk j, the other roles on further
      chunks) — chunk-sized sweeps, a few launches each;
-  3. if the pair times show no clearly fast pair, allocate more spares
-     (bounded) first;
+  3. if the pair times show no clearly fast pair (the pool sits in one
+     physical group), allocate more chunks, `spare` at a time, and time each
+     new one against chunk 0 only, until a group FAST_REF faster than chunk
+     0's shows or the pool holds MAX_CHUNKS / the budget;
   4. candidate assignments: the allocation order, up to COMPOSITES
      greedy ones (seeded by each of the fastest pairs, completed with the
      fastest disjoint pairs; theta / momentum from the pairs, the other roles
-     from the remaining chunks in allocation order); each is mapped and timed
+     from the remaining chunks in allocation order) and up to COMPOSITES from
+     the times against chunk 0 (its group for one role, the fastest group for
+     the other: ref_candidates); each is mapped and timed
      at FULL size — chunk-pair times only rank the seeds; and, competing
      with them, the roles plus TORCH_EXTRA more vectors allocated plainly by
      torch, with up to TORCH_PAIRINGS (theta, mom) pairings among them (on
@@ -583,6 +587,20 @@ def one_candidates(chunk_ms, per, limit=ONE_COMPOSITES):
     return cands
 
 
+ONE_SPREAD = 0.98  # place_one: two groups of chunks show as this much spread
+
+
+def _one_found(chunk_ms, per):
+    """place_one's stop rule: the chunk times split into two groups (fastest
+    ONE_SPREAD below the slowest) with at least `per` chunks in the faster
+    (at or below the midpoint)."""
+    lo, hi = min(chunk_ms), max(chunk_ms)
+    if not lo < ONE_SPREAD * hi:
+        return False
+    mid = 0.5 * (lo + hi)
+    return sum(t <= mid for t in chunk_ms) >= per
+
+
 def place_one(n, device, launcher, time_launch, budget_bytes, spare=None, pool_key=None,
               beat_ms=None):
     """One WRITTEN vector (n fp32 elements) from physical chunks, for a sweep
@@ -595,7 +613,8 @@ def place_one(n, device, launcher, time_launch, budget_bytes, spare=None, pool_k
 
       1. allocate per + spare chunks (each also mapped alone);
       2. time the sweep into every chunk (chunk-sized: the reads are the
-         inputs' leading slices);
+         inputs' leading slices); while the times show no second group,
+         allocate 2 per more (up to MAX_CHUNKS / the budget);
       3. map composites of the fastest chunks (the per fastest, then the next
          ONE_COMPOSITES - 1 windows of the ranking) and the allocation order,
          and time each at FULL size.
@@ -629,6 +648,13 @@ def place_one(n, device, launcher, time_launch, budget_bytes, spare=None, pool_k
     try:
         ch.add(per + spare)
         chunk_ms = [time_launch(launcher(v[:k])) for v in ch.views]
+        # all chunks alike: they share one physical group — add more until
+        # another group shows (as place() does), within MAX_CHUNKS / the budget
+        while not _one_found(chunk_ms, per) and spare > 0 and \
+                len(ch.views) + spare <= MAX_CHUNKS and (len(ch.views) + spare) * cb <= budget_bytes:
+            k1 = len(ch.views)
+            ch.add(spare)
+            chunk_ms += [time_launch(launcher(v[:k])) for v in ch.views[k1:]]
         for ids in one_candidates(chunk_ms, per):
             m = Mapping(dev_index, [ch.handles[i] for i in ids], cb, n)
             t = m.tensor()

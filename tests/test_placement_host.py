@@ -166,3 +166,11 @@ def test_ref_candidates_pair_chunk0s_group_with_the_fast_group(names, per):
     assert cands[1]["theta"][0] == 0 and cands[1]["mom"] == fastest
     # no split: allocation order only
     assert P.ref_candidates({j: 1.0 for j in range(1, nchunks)}, nchunks, names, per) == cands[:1]
+
+
+def test_one_found_needs_a_spread_and_per_fast_chunks():
+    """placement._one_found (place_one's escalation stop rule)."""
+    assert P._one_found([0.30, 0.31, 0.295, 0.311], 2)          # 5 % spread, 2 fast
+    assert not P._one_found([0.30, 0.301, 0.302, 0.3005], 1)    # one group
+    assert not P._one_found([0.29, 0.31, 0.312, 0.311], 2)      # only one fast chunk
+    assert P._one_found([0.29, 0.31], 1)
