@@ -668,7 +668,7 @@ def place_one(n, device, launcher, time_launch, budget_bytes, spare=None, pool_k
         ch.release()
     won = beat_ms is None or best_ms < beat_ms
     info = {"allocator": "vmm" if won else "torch", "kept": "chunks" if won else "torch",
-            "chunk_mb": cb >> 20, "chunks_per_vector": per, "chunks_allocated": per + spare,
+            "chunk_mb": cb >> 20, "chunks_per_vector": per, "chunks_allocated": len(chunk_ms),
             "chunk_ms": [round(t, 4) for t in chunk_ms], "composites_ms": comp_ms,
             "chosen_ms": round(best_ms, 4), "chunks": chosen if won else [],
             "beat_ms": None if beat_ms is None else round(beat_ms, 4), "reused": False,
