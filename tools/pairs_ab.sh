@@ -22,6 +22,7 @@ print(json.dumps({"mode": sys.argv[1], "method": sys.argv[2], "round": int(sys.a
                   "chosen_ms": p.get("chosen_ms"), "kept": p.get("kept"),
                   "search_s": p.get("search_seconds", p.get("seconds")),
                   "pairs_timed": p.get("pairs_timed"), "chunks": p.get("chunks_allocated"),
+                  "rounds": p.get("escalation_rounds"),
                   "composites_ms": p.get("composites_ms"), "torch_ms": p.get("torch_ms")}))
 PY
       tail -1 $OUT
