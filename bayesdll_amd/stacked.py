@@ -256,6 +256,9 @@ class _StackedSampler:
             # (scratch on plain allocations, as the stacked state's own vectors)
             self.state.launch_cfg = K.autotune_once(self.state.n, self.state.device,
                                                     self.tune_method, placed=False)
+            if self.state.launch_cfg is not None:  # the collect steps' own geometry
+                self.state.collect_cfg = K.collect_config(self.state.n, self.state.device,
+                                                          self.tune_method)
         self.criterion = criterion or torch.nn.CrossEntropyLoss()
         self.step_count = 0
         self.draws = 0
