@@ -174,3 +174,18 @@ def test_one_found_needs_a_spread_and_per_fast_chunks():
     assert not P._one_found([0.30, 0.301, 0.302, 0.3005], 1)    # one group
     assert not P._one_found([0.29, 0.31, 0.312, 0.311], 2)      # only one fast chunk
     assert P._one_found([0.29, 0.31], 1)
+
+
+def test_ref_found_wants_the_best_level_not_the_middle_one():
+    """placement._ref_found (the escalation's stop rule): a second group at least
+    FAST_REF faster than chunk 0's own group stops it; a middle level (~4-5 %)
+    or a single group does not."""
+    slow = {j: 0.51 + 0.001 * (j % 3) for j in range(1, 8)}
+    assert not P._ref_found(slow, 2)                                    # one group
+    mid = {**slow, 8: 0.488, 9: 0.489}                            # ~4.3 % faster
+    assert not P._ref_found(mid, 2)
+    best = {**slow, 8: 0.476, 9: 0.477}                           # ~6.8 % faster
+    assert P._ref_found(best, 2)
+    assert not P._ref_found({**slow, 8: 0.476}, 2)               # one fast chunk < per
+    # chunk 0 alone in its group (per = 1): compared with the slowest time
+    assert P._ref_found({1: 0.47, 2: 0.51}, 1)
