@@ -199,73 +199,12 @@ class _FakeLaunch:
         pass
 
 
-def test_place_escalates_until_another_group_shows(monkeypatch):
-    """placement.place end to end on the host with fake chunks and a timing
-    model in which chunks 0-19 form one physical group and 20-39 another
-    (theta / mom in different groups: 0.96, same group: 1.05).  The first pool
-    (8 chunks, all pairs) is one group; the escalation adds 4 chunks a round,
-    each timed against chunk 0, until chunks 20-23 show; the kept set pairs
-    the two groups."""
+@pytest.fixture
+def fake_chunks(monkeypatch):
+    """placement's chunk allocator and mappings replaced by host fakes: each
+    chunk / composite is a CPU tensor; returns {data_ptr: chunk ids}."""
     import torch
-    monkeypatch.setattr(P, "CHUNK_TARGET", 2 << 20)     # 2-MiB chunks: per = 2 below
-    chunks_of = {}                                       # data_ptr -> chunk ids
-
-    class FakeMapping:
-        def __init__(self, dev_index, handles, chunk_bytes, nelem, adopt=None):
-            self.owner = self.role = None
-            self.handles, self.nelem = list(handles), nelem
-            self.va, self.total = 1, len(handles) * chunk_bytes
-
-        def tensor(self):
-            t = torch.zeros(self.nelem)
-            chunks_of[t.data_ptr()] = self.handles
-            return t
-
-    class FakeChunks:
-        def __init__(self, dev_index, chunk_bytes):
-            self.chunk_bytes, self.handles, self.views = chunk_bytes, [], []
-
-        def add(self, k):
-            for _ in range(k):
-                h = len(self.handles)
-                self.handles.append(h)
-                self.views.append(FakeMapping(0, [h], self.chunk_bytes,
-                                              self.chunk_bytes // 4).tensor())
-
-        def release(self):
-            self.views, self.handles = [], []
-
-    monkeypatch.setattr(P, "Mapping", FakeMapping)
-    monkeypatch.setattr(P, "_Chunks", FakeChunks)
-
-    def ids(t):
-        return chunks_of[t.data_ptr()]
-
-    def time_launch(f):
-        th, mo = ids(f.roles["theta"]), ids(f.roles["mom"])
-        return sum(0.96 if a // 20 != b // 20 else 1.05 for a, b in zip(th, mo)) / len(th)
-
-    n = 1 << 20                                          # 4 MB: two 2-MiB chunks per vector
-    vecs, info = P.place(n, "cuda:0", ["theta", "mom"], lambda roles, m: _FakeLaunch(roles),
-                         time_launch, budget_bytes=1 << 34, with_torch=False)
-    assert info["chunks_per_vector"] == 2
-    assert info["chunks_allocated"] == 24 and info["escalation_rounds"] == 4
-    assert info["pairs_timed"] == 8 * 7 + 16             # first pool all pairs, then vs chunk 0
-    assert len(info["ref_ms"]) == 23
-    assert info["chosen_ms"] == pytest.approx(0.96) and info["kept"] == "search"
-    th, mo = info["theta_chunks"], info["mom_chunks"]
-    groups = ({c // 20 for c in th}, {c // 20 for c in mo})
-    assert groups in (({0}, {1}), ({1}, {0})), (th, mo)
-    assert set(vecs) == {"theta", "mom"} and all(v.numel() == n for v in vecs.values())
-
-
-def test_place_one_escalates_until_a_faster_group_shows(monkeypatch):
-    """placement.place_one on the host with fake chunks: chunks 0-9 write at
-    0.31 ms, 10+ at 0.29 (the group opposite the draw's reads).  The first 6
-    chunks are all slow; two rounds of 4 reach chunks 10-13; the composite is
-    built from them."""
-    import torch
-    monkeypatch.setattr(P, "CHUNK_TARGET", 2 << 20)
+    monkeypatch.setattr(P, "CHUNK_TARGET", 2 << 20)     # 2-MiB chunks
     chunks_of = {}
 
     class FakeMapping:
@@ -295,9 +234,70 @@ def test_place_one_escalates_until_a_faster_group_shows(monkeypatch):
 
     monkeypatch.setattr(P, "Mapping", FakeMapping)
     monkeypatch.setattr(P, "_Chunks", FakeChunks)
+    return chunks_of
+
+
+def test_place_escalates_until_another_group_shows(fake_chunks):
+    """placement.place end to end on the host with fake chunks and a timing
+    model in which chunks 0-19 form one physical group and 20-39 another
+    (theta / mom in different groups: 0.96, same group: 1.05).  The first pool
+    (8 chunks, all pairs) is one group; the escalation adds 4 chunks a round,
+    each timed against chunk 0, until chunks 20-23 show; the kept set pairs
+    the two groups."""
+    def time_launch(f):
+        th, mo = fake_chunks[f.roles["theta"].data_ptr()], fake_chunks[f.roles["mom"].data_ptr()]
+        return sum(0.96 if a // 20 != b // 20 else 1.05 for a, b in zip(th, mo)) / len(th)
+
+    n = 1 << 20                                          # 4 MB: two 2-MiB chunks per vector
+    vecs, info = P.place(n, "cuda:0", ["theta", "mom"], lambda roles, m: _FakeLaunch(roles),
+                         time_launch, budget_bytes=1 << 34, with_torch=False)
+    assert info["chunks_per_vector"] == 2 and info["pairs"] == "all"
+    assert info["chunks_allocated"] == 24 and info["escalation_rounds"] == 4
+    assert info["pairs_timed"] == 8 * 7 + 16             # first pool all pairs, then vs chunk 0
+    assert len(info["ref_ms"]) == 23
+    assert info["chosen_ms"] == pytest.approx(0.96) and info["kept"] == "search"
+    assert info["retimed_ms"] is None                    # RETIME off by default
+    th, mo = info["theta_chunks"], info["mom_chunks"]
+    groups = ({c // 20 for c in th}, {c // 20 for c in mo})
+    assert groups in (({0}, {1}), ({1}, {0})), (th, mo)
+    assert set(vecs) == {"theta", "mom"} and all(v.numel() == n for v in vecs.values())
+
+
+def test_place_retimes_the_finalists(fake_chunks, monkeypatch):
+    """BDL_PLACEMENT_RETIME=3: the three fastest candidates are timed twice
+    more and the best MEAN wins — the composite that was lucky once (0.90,
+    then 0.99) loses to one that is fast every time (0.95)."""
+    monkeypatch.setattr(P, "RETIME", 3)
+    order, calls = [], {}
+    seq = {0: [0.90, 0.99, 0.99], 1: [0.95, 0.95, 0.95]}  # by first appearance
 
     def time_launch(f):
-        ch = chunks_of[f.roles["out"].data_ptr()]
+        th, mo = fake_chunks[f.roles["theta"].data_ptr()], fake_chunks[f.roles["mom"].data_ptr()]
+        if len(th) == 1:                                 # chunk pairs: two groups of 4
+            return 0.5 if th[0] // 4 != mo[0] // 4 else 0.55
+        key = (tuple(th), tuple(mo))
+        if key not in calls:
+            order.append(key)
+            calls[key] = 0
+        calls[key] += 1
+        return seq.get(order.index(key), [1.0] * 3)[calls[key] - 1]
+
+    n = 1 << 20
+    _, info = P.place(n, "cuda:0", ["theta", "mom"], lambda roles, m: _FakeLaunch(roles),
+                      time_launch, budget_bytes=1 << 34, with_torch=False)
+    assert info["composites_ms"][:2] == [0.9, 0.95]
+    assert info["retimed_ms"][:2] == [pytest.approx(0.96), pytest.approx(0.95)]  # first-round order
+    assert info["chosen_ms"] == pytest.approx(0.95)
+    assert [list(order[1][0]), list(order[1][1])] == [info["theta_chunks"], info["mom_chunks"]]
+
+
+def test_place_one_escalates_until_a_faster_group_shows(fake_chunks):
+    """placement.place_one on the host with fake chunks: chunks 0-9 write at
+    0.31 ms, 10+ at 0.29 (the group opposite the draw's reads).  The first 6
+    chunks are all slow; two rounds of 4 reach chunks 10-13; the composite is
+    built from them."""
+    def time_launch(f):
+        ch = fake_chunks[f.roles["out"].data_ptr()]
         return sum(0.29 if c >= 10 else 0.31 for c in ch) / len(ch)
 
     n = 1 << 20
