@@ -113,7 +113,7 @@ def _time_launch(launch, device, reps=5):
 PLACEMENT_BPC = {"csghmc": 1, "sgld": 2, "adam": 2}
 
 
-def placed_vectors(n, device, names, method):
+def placed_vectors(n, device, names, method, place_grad=False):
     """Allocate the chain's swept fp32 vectors (`names` among theta, grad, mom,
     prior, extra state), zeroed.  With `method` (the sampler's kernel family)
     and vectors of >= PLACEMENT_MIN_ELEMS, they are built from physical chunks
@@ -133,19 +133,24 @@ def placed_vectors(n, device, names, method):
     from . import placement as P
     free, _ = torch.cuda.mem_get_info(device)
     runs_by_n = {}
-    # the gradient is read-only in every sweep and its placement never shows
-    # (profiles/round2/placement/role_mix/): a plain allocation, outside the
-    # placed set, so the set's key does not depend on the gradient mode (a
-    # "tensor"-mode state drops it at once)
-    pnames = [nm for nm in names if nm != "grad"]
-    grad = torch.zeros(n, **f32) if "grad" in names else None
+    # the gradient is read-only in every sweep; its memory moved the sweep by
+    # 0.3 % on one box (profiles/round2/placement/role_mix/) and ~2 % on
+    # another (tools/grad_spread.py, round 3).  A flat gradient vector the
+    # state keeps (place_grad: "flat" gradient mode) is placed with the set —
+    # chosen after the (theta, mom) pairing; a "tensor"-mode state, whose
+    # gradients are autograd's own, gets a plain scratch vector it drops at
+    # once, outside the set (so the set's key says which kind it is)
+    place_grad = place_grad and "grad" in names and os.environ.get("BDL_PLACEMENT_GRAD", "1") != "0"
+
+    pnames = [nm for nm in names if nm != "grad" or place_grad]
+    grad = torch.zeros(n, **f32) if "grad" in names and not place_grad else None
     per, cb = P.chunk_geometry(n)
     gsrc = grad if grad is not None and cb // 4 <= n else torch.zeros(max(n, cb // 4), **f32)
 
     def launcher(roles, m):
         if m not in runs_by_n:
             runs_by_n[m] = build_runs([0], [m], [L.ATTR_PRIOR], m).to(device)
-        return _placement_launcher(method, dict(roles, grad=gsrc[:m]), m, device, runs_by_n[m])
+        return _placement_launcher(method, {"grad": gsrc[:m], **roles}, m, device, runs_by_n[m])
 
     from . import kernels as K
     # the probe kernel's depth is fixed at 4; workgroups per CU: the method's
@@ -267,7 +272,8 @@ class FlatState:
         # scratch gradient vector, freed after the choice)
         names_ = ["theta", "grad"] + (["mom"] if need_mom else []) + \
             (["prior"] if need_prior else []) + list(extra)
-        vecs, self.placement_info = placed_vectors(self.n, dev, names_, placement)
+        vecs, self.placement_info = placed_vectors(self.n, dev, names_, placement,
+                                                   place_grad=self.grad_mode == "flat")
         if self.grad_mode == "tensor":
             del vecs["grad"]
         # further per-element state of the sampler (e.g. Adam's m, v and the
@@ -327,9 +333,12 @@ class FlatState:
     @classmethod
     def from_segments(cls, segments, readout_name, *, bias="informative", device="cuda",
                       need_prior=False, need_mom=True, need_noise=False, init=None,
-                      placement=None, extra=()):
+                      placement=None, extra=(), place_grad=True):
         """Flat chain state for a segment table alone (no nn.Module): the
-        benchmark and kernel tests use it with synthetic vectors."""
+        benchmark and kernel tests use it with synthetic vectors.
+        place_grad=False: its gradient vector stays outside the placed set (as
+        a "tensor"-gradient-mode chain's scratch, e.g. the autotune scratch of
+        such a chain, whose placed set that chain then takes)."""
         self = cls.__new__(cls)
         self.names = [nm for nm, _ in segments]
         self.shapes = [tuple(s) for _, s in segments]
@@ -348,7 +357,8 @@ class FlatState:
         names_ = (["theta"] if init is None else []) + ["grad"] + (["mom"] if need_mom else []) \
             + (["prior"] if need_prior else []) + list(extra)
         vecs, self.placement_info = placed_vectors(
-            self.n, self.device, names_, placement if init is None else None)
+            self.n, self.device, names_, placement if init is None else None,
+            place_grad=place_grad)
         self.extra = {nm: vecs[nm].zero_() for nm in extra}
         self.theta = vecs["theta"] if init is None else init
         self.grad_mode = "flat"

@@ -356,6 +356,25 @@ def _ref_split(times0, per):
     return slow, fast
 
 
+def with_grad(assign, rank, names, per, nchunks):
+    """`assign` (chunk ids per role) with the gradient on the best-ranked
+    `per` chunks of `rank` that theta / mom do not use, the other roles
+    re-filled from the remaining chunks in allocation order."""
+    used = set(assign["theta"]) | set(assign["mom"])
+    grad = [k for k in rank if k not in used][:per]
+    rest = [k for k in range(nchunks) if k not in used and k not in grad]
+    out, r = {}, 0
+    for nm in names:
+        if nm in ("theta", "mom"):
+            out[nm] = list(assign[nm])
+        elif nm == "grad":
+            out[nm] = grad
+        else:
+            out[nm] = rest[r * per:(r + 1) * per]
+            r += 1
+    return out
+
+
 def _ref_found(times0, per):
     """The escalation's stop rule: a split (_ref_split) whose fastest chunk is
     FAST_REF faster than chunk 0's group (the median of its slow times; the
@@ -452,14 +471,21 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
     try:
         ch.add(nroles * per + spare)
 
-        def roles_for(i, j):
-            rest = [k for k in range(len(ch.views)) if k not in (i, j)]
+        # a placed gradient ("grad" among the roles) is left out of the pair
+        # timings (the launcher supplies its own) and chosen after them
+        grad_role = "grad" in names
+
+        def roles_for(i, j, g=None):
+            rest = [k for k in range(len(ch.views)) if k not in (i, j, g)]
             out, r = {}, 0
             for q, nm in enumerate(names):
                 if q == it:
                     out[nm] = ch.views[i]
                 elif q == im:
                     out[nm] = ch.views[j]
+                elif nm == "grad":
+                    if g is not None:
+                        out[nm] = ch.views[g]
                 else:
                     out[nm] = ch.views[rest[r]]
                     r += 1
@@ -502,6 +528,22 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
         for c in ref_candidates(times0(), len(ch.views), names, per):
             if c not in cands:
                 cands.append(c)
+        grad_ms = {}
+        if search and grad_role and times:
+            # the gradient's chunks: every other chunk timed as the gradient of
+            # the fastest (theta, mom) pair — on some boxes the read-only
+            # stream's memory moves the sweep by ~2 % (tools/grad_spread.py)
+            bi, bj = min(times, key=times.get)
+            for g in range(len(ch.views)):
+                if g not in (bi, bj):
+                    grad_ms[g] = time_launch(launcher(roles_for(bi, bj, g), nchunk))
+            rank = sorted(grad_ms, key=grad_ms.get)
+            cands = cands[:1] + [with_grad(c, rank, names, per, len(ch.views)) for c in cands[1:]]
+            uniq = []
+            for c in cands:
+                if c not in uniq:
+                    uniq.append(c)
+            cands = uniq
         # the fastest RETIME candidates stay alive (mapped) for a second timing
         # round; the others are dropped (unmapped) as soon as they lose
         top = []  # [ms, source, vectors, mappings, chunk ids per role]
@@ -568,7 +610,8 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
     pair_ms = sorted(times.values()) or [float("nan")]
     info = {"allocator": "torch" if best_src == "torch" else "vmm", "search": bool(search), "chunk_mb": cb >> 20,
             "chunks_per_vector": per, "chunks_allocated": nk, "pairs": pairs if search else None,
-            "escalation_rounds": rounds,
+            "escalation_rounds": rounds, "grad_timed": len(grad_ms),
+            "grad_chunks": chosen.get("grad") if grad_role else None,
             "ref_ms": [round(t, 4) for _, t in sorted(times0().items())],
             "pairs_timed": len(times), "pair_ms_min": round(pair_ms[0], 4),
             "pair_ms_median": round(pair_ms[len(pair_ms) // 2], 4),

@@ -391,7 +391,8 @@ def main():
         # (its scratch vectors placed like the chain's: their parked set becomes
         # the chain's, bayesdll_amd.placement)
         best, tuned, cbest, ctuned = K.autotune(n_all, device=local, method=tune_method,
-                                                placed=a.placement, collect=True)
+                                                placed=a.placement, collect=True,
+                                                place_grad=a.grad_mode == "flat")
         launch = {"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
                   "autotuned": True,
                   "candidates_ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4) for c, t in tuned.items()},
@@ -407,7 +408,8 @@ def main():
     sgld = a.method == "sgld" or adam  # adam shares config 3's state/driver shape
     st = FlatState.from_segments(segs, readout, device=dev, need_prior=sgld,
                                  placement=tune_method if a.placement else None,
-                                 extra=("adam_m", "adam_v", "sgd_buf") if adam else ())
+                                 extra=("adam_m", "adam_v", "sgd_buf") if adam else (),
+                                 place_grad=a.grad_mode == "flat")
     if launch.get("autotuned"):
         st.launch_cfg, st.collect_cfg = best, cbest
     gen = torch.Generator(device=dev).manual_seed(42 + rank)

@@ -634,14 +634,19 @@ def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
             info = st.placement_info
             per, cb = P.chunk_geometry(st.n)
             assert info["chunks_per_vector"] == per == 1
-            # the placed set is theta + mom; the read-only gradient is a plain allocation
-            k0 = 2 * per + 2 * per  # the first pool: every ordered pair timed
+            # the placed set is theta + grad + mom (a flat-gradient state's
+            # gradient is placed too, chosen after the theta / mom pairing)
+            k0 = 3 * per + 2 * per  # the first pool: every ordered pair timed
             assert info["chunks_allocated"] >= k0
             # chunks added by the escalation are timed against chunk 0 only
             assert info["pairs_timed"] == k0 * (k0 - 1) + (info["chunks_allocated"] - k0)
             assert len(info["ref_ms"]) == info["chunks_allocated"] - 1
             assert info["chunks_allocated"] <= P.MAX_CHUNKS
-            nt = 2 + P.TORCH_EXTRA
+            assert info["grad_timed"] == info["chunks_allocated"] - 2
+            if info["kept"] != "torch":
+                assert len(info["grad_chunks"]) == per and \
+                    not set(info["grad_chunks"]) & set(info["theta_chunks"] + info["mom_chunks"])
+            nt = 3 + P.TORCH_EXTRA
             assert len(info["torch_ms"]) == min(P.TORCH_PAIRINGS, nt * (nt - 1) // 2)
             assert len(info["composites_ms"]) >= 2
             assert info["chosen_ms"] == min(info["composites_ms"] + info["torch_ms"])

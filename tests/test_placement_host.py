@@ -306,3 +306,37 @@ def test_place_one_escalates_until_a_faster_group_shows(fake_chunks):
     assert buf is not None and buf.numel() == n
     assert info["chunks_allocated"] == 14 == len(info["chunk_ms"])
     assert info["chosen_ms"] == pytest.approx(0.29) and all(c >= 10 for c in info["chunks"])
+
+
+def test_with_grad_takes_the_best_free_chunks():
+    """placement.with_grad: the gradient gets the best-ranked chunks theta / mom
+    leave free; the other roles are re-filled in allocation order."""
+    a = {"theta": [0, 1], "grad": [2, 3], "mom": [4, 5], "prior": [6, 7]}
+    out = P.with_grad(a, [4, 9, 1, 8, 2], ["theta", "grad", "mom", "prior"], 2, 10)
+    assert out == {"theta": [0, 1], "grad": [9, 8], "mom": [4, 5], "prior": [2, 3]}
+
+
+def test_place_times_the_gradient_after_the_pair(fake_chunks):
+    """A placed gradient ("grad" among the roles) is left out of the pair
+    timings and then timed on every other chunk against the fastest pair; the
+    candidates put it on the fastest chunks."""
+    seen_grad = []
+
+    def time_launch(f):
+        th, mo = fake_chunks[f.roles["theta"].data_ptr()], fake_chunks[f.roles["mom"].data_ptr()]
+        g = f.roles.get("grad")
+        gc = fake_chunks[g.data_ptr()] if g is not None else None
+        seen_grad.append(gc is not None)
+        t = sum(0.96 if a // 4 != b // 4 else 1.05 for a, b in zip(th, mo)) / len(th)
+        if gc is not None:                                # chunks 6, 7 the best gradient home
+            t -= 0.01 * sum(c in (6, 7) for c in gc) / len(gc)
+        return t
+
+    n = 1 << 20
+    vecs, info = P.place(n, "cuda:0", ["theta", "grad", "mom"], lambda roles, m: _FakeLaunch(roles),
+                         time_launch, budget_bytes=1 << 34, with_torch=False)
+    k0 = 3 * 2 + 2 * 2
+    assert not any(seen_grad[:k0 * (k0 - 1)])             # pair timings: no placed gradient
+    assert info["grad_timed"] == info["chunks_allocated"] - 2
+    assert sorted(info["grad_chunks"]) == [6, 7]
+    assert set(vecs) == {"theta", "grad", "mom"}
