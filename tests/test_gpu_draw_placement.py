@@ -54,7 +54,8 @@ def test_draw_buffer_choice_changes_nothing_but_the_buffer(monkeypatch):
     assert ch is not None and "error" not in ch, ch
     assert d1.placement["kept"] in ("torch", "chunks")
     if d1.placement["kept"] == "chunks":
-        assert ch["chosen_ms"] < min(d1.placement["torch_ms"])
+        # kept only when faster (info values are rounded to 0.1 us: a tie can show)
+        assert ch["chosen_ms"] <= min(d1.placement["torch_ms"])
     for a, b in zip(th0, th1):
         assert torch.equal(a, b)
     for a, b in zip(outs0, outs1):
