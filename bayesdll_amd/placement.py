@@ -286,6 +286,29 @@ def _has_fast_pair(times):
     return t[0] < FAST_PAIR * t[len(t) // 2]
 
 
+def _fast_pairs_found(times, per):
+    """The first pool's stop rule: `per` DISJOINT (theta, mom) chunk pairs each
+    FAST_PAIR below the median pair — what a composite needs.  One fast pair
+    is not enough when per > 1: with a single chunk of the other group in the
+    pool every fast pair shares it, and the best composite pairs one fast and
+    one slow chunk (~1.0 ms where two fast pairs give ~0.96)."""
+    if not times:
+        return False
+    vals = sorted(times.values())
+    cut = FAST_PAIR * vals[len(vals) // 2]
+    used, got = set(), 0
+    for (i, j) in sorted(times, key=times.get):
+        if times[(i, j)] >= cut:
+            break
+        if i in used or j in used:
+            continue
+        used.update((i, j))
+        got += 1
+        if got == per:
+            return True
+    return False
+
+
 def candidate_assignments(times, nchunks, names, per, limit=COMPOSITES):
     """Chunk ids per role for the full-size candidates: the allocation order
     first, then up to `limit` greedy assignments — each seeded by one of the
@@ -504,7 +527,7 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
                 for j in range(len(ch.views)):
                     if i != j:
                         times[(i, j)] = time_launch(launcher(roles_for(i, j), nchunk))
-            found = _has_fast_pair(times.values()) if pairs == "all" else _ref_found(times0(), per)
+            found = _fast_pairs_found(times, per) if pairs == "all" else _ref_found(times0(), per)
             # no fast pair yet: the pool's chunks sit in one physical group (on
             # some boxes a group spans more than 16 chunks of 586 MB: a 16-chunk
             # all-pairs search kept 1.03-1.04 ms where 28 chunks reached 0.96,

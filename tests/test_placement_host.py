@@ -340,3 +340,36 @@ def test_place_times_the_gradient_after_the_pair(fake_chunks):
     assert info["grad_timed"] == info["chunks_allocated"] - 2
     assert sorted(info["grad_chunks"]) == [6, 7]
     assert set(vecs) == {"theta", "grad", "mom"}
+
+
+def test_fast_pairs_found_needs_per_disjoint_fast_pairs():
+    """placement._fast_pairs_found: with one chunk of the other group in the
+    pool every fast pair shares it — not enough for a two-chunk composite."""
+    def times_for(groups):
+        k = len(groups)
+        return {(i, j): (0.48 if groups[i] != groups[j] else 0.52)
+                for i in range(k) for j in range(k) if i != j}
+    one_b = times_for([0, 0, 0, 0, 0, 0, 0, 1])
+    assert P._fast_pairs_found(one_b, 1)
+    assert not P._fast_pairs_found(one_b, 2)
+    two_b = times_for([0, 0, 0, 0, 0, 0, 1, 1])
+    assert P._fast_pairs_found(two_b, 2)
+    assert not P._fast_pairs_found(times_for([0] * 8), 1)
+    assert not P._fast_pairs_found({}, 1)
+
+
+def test_place_escalates_when_the_pool_has_one_chunk_of_the_other_group(fake_chunks):
+    """First pool: chunks 0-6 one group, chunk 7 the other — fast pairs exist
+    but all share chunk 7; the search escalates instead of keeping a fast /
+    slow composite."""
+    def grp(c):
+        return 1 if c == 7 or c >= 12 else 0
+
+    def time_launch(f):
+        th, mo = fake_chunks[f.roles["theta"].data_ptr()], fake_chunks[f.roles["mom"].data_ptr()]
+        return sum(0.48 if grp(a) != grp(b) else 0.52 for a, b in zip(th, mo)) / len(th)
+
+    _, info = P.place(1 << 20, "cuda:0", ["theta", "mom"], lambda roles, m: _FakeLaunch(roles),
+                      time_launch, budget_bytes=1 << 34, with_torch=False)
+    assert info["escalation_rounds"] >= 1
+    assert info["chosen_ms"] == pytest.approx(0.48)
