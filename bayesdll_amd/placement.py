@@ -77,8 +77,10 @@ FAST_PAIR = 0.97         # a pair this much faster than the median pair is worth
 # when the first pool shows no fast pair, chunks are added `spare` at a time and
 # each new one is timed against chunk 0 only, until one group is this much
 # faster than chunk 0's own (the best of the three pairing levels, DESIGN.md §4,
-# not the middle one) or the pool holds MAX_CHUNKS / the budget
-FAST_REF = 0.94
+# not the middle one: at chunk size the best level times 5-7 % below chunk 0's
+# group, the middle one ~3.5 %, profiles/round3/aux/chunk_matrix/) or the pool
+# holds MAX_CHUNKS / the budget
+FAST_REF = 0.95
 MAX_CHUNKS = int(os.environ.get("BDL_PLACEMENT_MAX_CHUNKS", "64"))
 # > 1: the fastest RETIME candidates (chunk composites or plain pairings) are
 # timed twice more, interleaved, and the best mean wins (A/B knob)
@@ -399,15 +401,18 @@ def with_grad(assign, rank, names, per, nchunks):
 
 
 def _ref_found(times0, per):
-    """The escalation's stop rule: a split (_ref_split) whose fastest chunk is
-    FAST_REF faster than chunk 0's group (the median of its slow times; the
-    slowest time when the group is chunk 0 alone)."""
+    """The escalation's stop rule: a split (_ref_split) whose `per` fastest
+    chunks are all FAST_REF faster than chunk 0's group (the median of its
+    slow times; the slowest time when the group is chunk 0 alone)."""
     split = _ref_split(times0, per)
     if split is None:
         return False
     slow, fast = split
     ref = sorted(times0[j] for j in slow)[len(slow) // 2] if slow else max(times0.values())
-    return times0[fast[0]] < FAST_REF * ref
+    # the per-th fastest too: a midpoint split with one truly fast chunk can
+    # count a slow-group straggler as the second (seen on a box: 0.4819 and
+    # 0.5023 against a group at 0.503-0.524 ms)
+    return times0[fast[per - 1]] < FAST_REF * ref
 
 
 def ref_candidates(times0, nchunks, names, per, limit=COMPOSITES):

@@ -178,7 +178,7 @@ def test_one_found_needs_a_spread_and_per_fast_chunks():
 
 def test_ref_found_wants_the_best_level_not_the_middle_one():
     """placement._ref_found (the escalation's stop rule): a second group at least
-    FAST_REF faster than chunk 0's own group stops it; a middle level (~4-5 %)
+    FAST_REF faster than chunk 0's own group stops it; a middle level (~4.5 %)
     or a single group does not."""
     slow = {j: 0.51 + 0.001 * (j % 3) for j in range(1, 8)}
     assert not P._ref_found(slow, 2)                                    # one group
@@ -373,3 +373,14 @@ def test_place_escalates_when_the_pool_has_one_chunk_of_the_other_group(fake_chu
                       time_launch, budget_bytes=1 << 34, with_torch=False)
     assert info["escalation_rounds"] >= 1
     assert info["chosen_ms"] == pytest.approx(0.48)
+
+
+def test_ref_found_does_not_count_a_straggler_as_the_second_fast_chunk():
+    """The box that showed it: one truly fast chunk (0.4819) and a slow-group
+    straggler just under the midpoint (0.5023) must not stop the escalation at
+    per = 2."""
+    t = {1: 0.5188, 2: 0.5203, 3: 0.5131, 4: 0.5174, 5: 0.5188, 6: 0.508, 7: 0.5023,
+         8: 0.5112, 9: 0.5044, 10: 0.5031, 11: 0.5072, 12: 0.5101, 13: 0.5178, 14: 0.5241,
+         15: 0.5122, 16: 0.5156, 17: 0.4819}
+    assert not P._ref_found(t, 2)
+    assert P._ref_found({**t, 18: 0.4835}, 2)
