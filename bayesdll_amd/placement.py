@@ -681,6 +681,12 @@ def one_candidates(chunk_ms, per, limit=ONE_COMPOSITES):
 
 
 ONE_SPREAD = 0.98  # place_one: two groups of chunks show as this much spread
+# place_one's first pool (the draw's chunk-sized timings are cheap: ~1 ms a
+# chunk) and its bar against the caller's best plain allocation: the per
+# fastest chunks must sum below ONE_BEAT x beat_ms (a composite times 2-5 %
+# above the sum of its chunk-sized sweeps, profiles/round3/final*/bench.log)
+ONE_POOL = 16
+ONE_BEAT = 0.96
 
 
 def _one_found(chunk_ms, per):
@@ -704,10 +710,11 @@ def place_one(n, device, launcher, time_launch, budget_bytes, spare=None, pool_k
     elements: the sweep's inputs are sliced to it); `time_launch(launch)` its
     median ms.
 
-      1. allocate per + spare chunks (each also mapped alone);
+      1. allocate max(per + spare, ONE_POOL) chunks (each also mapped alone);
       2. time the sweep into every chunk (chunk-sized: the reads are the
-         inputs' leading slices); while the times show no second group,
-         allocate 2 per more (up to MAX_CHUNKS / the budget);
+         inputs' leading slices); while the times show no second group, or
+         the per fastest chunks do not promise to beat `beat_ms`, allocate
+         `spare` more (up to MAX_CHUNKS / the budget);
       3. map composites of the fastest chunks (the per fastest, then the next
          ONE_COMPOSITES - 1 windows of the ranking) and the allocation order,
          and time each at FULL size.
@@ -732,18 +739,24 @@ def place_one(n, device, launcher, time_launch, budget_bytes, spare=None, pool_k
     per, cb = chunk_geometry(n)
     k = min(cb // 4, n)  # elements the chunk-sized sweeps write (a 1-chunk vector's chunk is rounded up)
     spare = (2 * per if spare is None else spare)
-    while spare > 0 and (per + spare) * cb > budget_bytes:
-        spare -= 1
-    if (per + spare) * cb > budget_bytes:
+    first = max(per + spare, min(ONE_POOL, MAX_CHUNKS))
+    while first > per and first * cb > budget_bytes:
+        first -= 1
+    if first * cb > budget_bytes:
         return None, {"allocator": "torch", "kept": "torch", "skipped": "over budget"}
     ch = _Chunks(dev_index, cb)
     best, best_ms, best_map, comp_ms = None, None, None, []
+
+    def enough(ms):
+        if not _one_found(ms, per):
+            return False
+        return beat_ms is None or sum(sorted(ms)[:per]) < ONE_BEAT * beat_ms
     try:
-        ch.add(per + spare)
+        ch.add(first)
         chunk_ms = [time_launch(launcher(v[:k])) for v in ch.views]
-        # all chunks alike: they share one physical group — add more until
-        # another group shows (as place() does), within MAX_CHUNKS / the budget
-        while not _one_found(chunk_ms, per) and spare > 0 and \
+        # all chunks alike (one physical group), or none promising to beat the
+        # plain allocation: add more, within MAX_CHUNKS / the budget
+        while not enough(chunk_ms) and spare > 0 and \
                 len(ch.views) + spare <= MAX_CHUNKS and (len(ch.views) + spare) * cb <= budget_bytes:
             k1 = len(ch.views)
             ch.add(spare)

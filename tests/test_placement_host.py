@@ -292,20 +292,34 @@ def test_place_retimes_the_finalists(fake_chunks, monkeypatch):
 
 
 def test_place_one_escalates_until_a_faster_group_shows(fake_chunks):
-    """placement.place_one on the host with fake chunks: chunks 0-9 write at
-    0.31 ms, 10+ at 0.29 (the group opposite the draw's reads).  The first 6
-    chunks are all slow; two rounds of 4 reach chunks 10-13; the composite is
-    built from them."""
+    """placement.place_one on the host with fake chunks: chunks 0-17 write at
+    0.31 ms, 18+ at 0.29 (the group opposite the draw's reads).  The first
+    pool (ONE_POOL = 16 chunks) is all slow; one round of 4 reaches chunks
+    18-19; the composite is built from them."""
     def time_launch(f):
         ch = fake_chunks[f.roles["out"].data_ptr()]
-        return sum(0.29 if c >= 10 else 0.31 for c in ch) / len(ch)
+        return sum(0.29 if c >= 18 else 0.31 for c in ch) / len(ch)
 
     n = 1 << 20
     buf, info = P.place_one(n, "cuda:0", lambda b: _FakeLaunch({"out": b}), time_launch,
                             budget_bytes=1 << 34)
     assert buf is not None and buf.numel() == n
-    assert info["chunks_allocated"] == 14 == len(info["chunk_ms"])
-    assert info["chosen_ms"] == pytest.approx(0.29) and all(c >= 10 for c in info["chunks"])
+    assert info["chunks_allocated"] == 20 == len(info["chunk_ms"])
+    assert info["chosen_ms"] == pytest.approx(0.29) and all(c >= 18 for c in info["chunks"])
+
+
+def test_place_one_escalates_until_the_plain_allocation_is_beaten(fake_chunks):
+    """Two groups inside the first pool (0.31 / 0.30 ms per chunk) but neither
+    promising against a plain allocation at 0.585 ms full size: the pool grows
+    until chunks at 0.28 appear (from chunk 24)."""
+    def time_launch(f):
+        ch = fake_chunks[f.roles["out"].data_ptr()]
+        return sum(0.28 if c >= 24 else (0.30 if c % 2 else 0.31) for c in ch) / len(ch)
+
+    buf, info = P.place_one(1 << 20, "cuda:0", lambda b: _FakeLaunch({"out": b}), time_launch,
+                            budget_bytes=1 << 34, beat_ms=0.585)
+    assert info["chunks_allocated"] == 28
+    assert info["chosen_ms"] == pytest.approx(0.28) and buf is not None
 
 
 def test_with_grad_takes_the_best_free_chunks():
