@@ -56,9 +56,11 @@ class PosteriorDraw:
         they change no result."""
         step = EVAL_STEP_BASE + self.count
 
-        def launch(buf):
-            K.posterior_sample(buf, mean, m2, var_mode=var_mode, ratio=ratio, seed=self.seed,
-                               chain=self.chain, step=step)
+        def launch(buf, off=0):
+            m = buf.numel()
+            K.posterior_sample(buf, mean[off:off + m], None if m2 is None else m2[off:off + m],
+                               var_mode=var_mode, ratio=ratio, seed=self.seed, chain=self.chain,
+                               step=step)
         buf, info = draw_buffer(self.theta, launch)
         self.placement = info or {}
         if buf is not self.theta:

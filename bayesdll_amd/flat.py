@@ -651,8 +651,8 @@ def draw_buffer(out, launch, candidates=DRAW_CANDIDATES):
     """Pick the posterior-draw output buffer (DESIGN.md §4 placement: the draw
     reads m1 / m2 and writes out, and runs 3-4 % faster with out in the
     physical group opposite to its reads, which only timing reveals).
-    `launch(buf)` runs the draw into `buf` (its inputs' leading buf.numel()
-    elements when buf is shorter than they are).  `out` and candidates - 1
+    `launch(buf, off=0)` runs the draw into `buf` with its inputs' elements
+    off .. off + buf.numel() (the whole inputs for a full-size buf).  `out` and candidates - 1
     fresh allocations of its size are each timed (median of 3); then, with
     BDL_PLACEMENT=search (the default), a vector built from physical chunks
     chosen by timing the draw into each (placement.place_one, parked and
@@ -674,7 +674,8 @@ def draw_buffer(out, launch, candidates=DRAW_CANDIDATES):
     from . import placement as P
     free, _ = torch.cuda.mem_get_info(out.device)
     try:
-        buf, pinfo = P.place_one(out.numel(), out.device, lambda b: (lambda: launch(b)),
+        buf, pinfo = P.place_one(out.numel(), out.device,
+                                 lambda b, off: (lambda: launch(b, off)),
                                  lambda f: _time_launch(f, out.device, 3),
                                  budget_bytes=int(0.25 * free), pool_key=("draw",),
                                  beat_ms=ms[best])

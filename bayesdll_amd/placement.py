@@ -663,21 +663,40 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
 ONE_COMPOSITES = 3  # full-size composites timed by place_one besides allocation order
 
 
-def one_candidates(chunk_ms, per, limit=ONE_COMPOSITES):
-    """Chunk lists for place_one's full-size composites: the `per` fastest
-    chunks of `chunk_ms` (ms per chunk, fastest first), then up to limit - 1
-    further windows of `per` consecutive chunks of that ranking, then the
-    allocation order; no list twice."""
-    ranked = sorted(range(len(chunk_ms)), key=lambda i: chunk_ms[i])
+def one_candidates(pos_ms, per, limit=ONE_COMPOSITES):
+    """Chunk lists for place_one's full-size composites from `pos_ms` (per
+    lists: position p's ms for every chunk — position p of the vector is swept
+    together with the inputs' p-th slice, so a chunk's time depends on where
+    it sits): candidate w takes, position by position, the w-th fastest chunk
+    not yet used; then the allocation order; no list twice."""
+    nch = len(pos_ms[0])
+    ranked = [sorted(range(nch), key=lambda i, p=p: pos_ms[p][i]) for p in range(per)]
     cands = []
     for w in range(limit):
-        ids = ranked[w:w + per]
+        used, ids = set(), []
+        for p in range(per):
+            free = [c for c in ranked[p] if c not in used]
+            if len(free) <= w:
+                break
+            ids.append(free[w])
+            used.add(free[w])
         if len(ids) == per and ids not in cands:
             cands.append(ids)
     order = list(range(per))
     if order not in cands:
         cands.append(order)
     return cands
+
+
+def _one_estimate(pos_ms, per):
+    """Greedy estimate of the best composite from per-position chunk times
+    (position by position, the fastest chunk not yet used)."""
+    nch, used, est = len(pos_ms[0]), set(), 0.0
+    for p in range(per):
+        c = min((c for c in range(nch) if c not in used), key=lambda c: pos_ms[p][c])
+        used.add(c)
+        est += pos_ms[p][c]
+    return est
 
 
 ONE_SPREAD = 0.98  # place_one: two groups of chunks show as this much spread
@@ -705,19 +724,21 @@ def place_one(n, device, launcher, time_launch, budget_bytes, spare=None, pool_k
     """One WRITTEN vector (n fp32 elements) from physical chunks, for a sweep
     whose other streams are fixed (the posterior draw: m1 / m2 given, out
     chosen; DESIGN.md §4 — it runs fastest with out in the physical group
-    opposite to its reads, which only timing reveals).  `launcher(buf)` returns
-    a zero-argument launch of the sweep writing `buf` (buf.numel() <= n
-    elements: the sweep's inputs are sliced to it); `time_launch(launch)` its
-    median ms.
+    opposite to its reads, which only timing reveals).  `launcher(buf, off)`
+    returns a zero-argument launch of the sweep writing `buf` with its inputs
+    from element `off` on (buf.numel() <= n - off elements); `time_launch(launch)`
+    its median ms.
 
       1. allocate max(per + spare, ONE_POOL) chunks (each also mapped alone);
-      2. time the sweep into every chunk (chunk-sized: the reads are the
-         inputs' leading slices); while the times show no second group, or
-         the per fastest chunks do not promise to beat `beat_ms`, allocate
-         `spare` more (up to MAX_CHUNKS / the budget);
-      3. map composites of the fastest chunks (the per fastest, then the next
-         ONE_COMPOSITES - 1 windows of the ranking) and the allocation order,
-         and time each at FULL size.
+      2. time the sweep into every chunk at every position p of the vector
+         (chunk-sized: the reads are the inputs' p-th slices — the sweep's
+         speed depends on the output's memory AND the inputs' at the same
+         offset); while the times show no second group, or the best
+         position-by-position estimate does not promise to beat `beat_ms`,
+         allocate `spare` more (up to MAX_CHUNKS / the budget);
+      3. map composites (one_candidates: position by position, the w-th
+         fastest free chunk) and the allocation order, and time each at FULL
+         size.
 
     The fastest composite is returned if it beats `beat_ms` (the caller's best
     plain allocation), else (None, info): the caller keeps its own buffer.
@@ -747,25 +768,33 @@ def place_one(n, device, launcher, time_launch, budget_bytes, spare=None, pool_k
     ch = _Chunks(dev_index, cb)
     best, best_ms, best_map, comp_ms = None, None, None, []
 
-    def enough(ms):
-        if not _one_found(ms, per):
-            return False
-        return beat_ms is None or sum(sorted(ms)[:per]) < ONE_BEAT * beat_ms
+    def enough(pos_ms):
+        if beat_ms is None:
+            return _one_found(pos_ms[0], per)
+        return _one_estimate(pos_ms, per) < ONE_BEAT * beat_ms
+
+    def time_chunks(views):
+        # position p: the chunk-sized sweep over the inputs' p-th slice (the
+        # last position's slice may be shorter than a chunk)
+        return [[time_launch(launcher(v[:min(k, n - p * k)], p * k)) for v in views]
+                for p in range(per)]
     try:
         ch.add(first)
-        chunk_ms = [time_launch(launcher(v[:k])) for v in ch.views]
+        pos_ms = time_chunks(ch.views)
         # all chunks alike (one physical group), or none promising to beat the
         # plain allocation: add more, within MAX_CHUNKS / the budget
-        while not enough(chunk_ms) and spare > 0 and \
+        while not enough(pos_ms) and spare > 0 and \
                 len(ch.views) + spare <= MAX_CHUNKS and (len(ch.views) + spare) * cb <= budget_bytes:
             k1 = len(ch.views)
             ch.add(spare)
-            chunk_ms += [time_launch(launcher(v[:k])) for v in ch.views[k1:]]
-        for ids in one_candidates(chunk_ms, per):
+            for p, more in enumerate(time_chunks(ch.views[k1:])):
+                pos_ms[p] += more
+        chunk_ms = pos_ms[0]
+        for ids in one_candidates(pos_ms, per):
             m = Mapping(dev_index, [ch.handles[i] for i in ids], cb, n)
             t = m.tensor()
             t.zero_()
-            ms = time_launch(launcher(t))
+            ms = time_launch(launcher(t, 0))
             comp_ms.append(round(ms, 4))
             if best_ms is None or ms < best_ms:
                 best, best_ms, best_map, chosen = t, ms, m, ids
@@ -775,7 +804,9 @@ def place_one(n, device, launcher, time_launch, budget_bytes, spare=None, pool_k
     won = beat_ms is None or best_ms < beat_ms
     info = {"allocator": "vmm" if won else "torch", "kept": "chunks" if won else "torch",
             "chunk_mb": cb >> 20, "chunks_per_vector": per, "chunks_allocated": len(chunk_ms),
-            "chunk_ms": [round(t, 4) for t in chunk_ms], "composites_ms": comp_ms,
+            "chunk_ms": [round(t, 4) for t in chunk_ms],
+            "chunk_ms_by_pos": [[round(t, 4) for t in row] for row in pos_ms],
+            "composites_ms": comp_ms,
             "chosen_ms": round(best_ms, 4), "chunks": chosen if won else [],
             "beat_ms": None if beat_ms is None else round(beat_ms, 4), "reused": False,
             "seconds": round(time.perf_counter() - t_start, 3),

@@ -239,8 +239,9 @@ def aux_kernels(st, reps=20):
     # the output buffer chosen as the Runners' posterior draws choose it
     # (flat.draw_buffer: the plain allocation and fresh ones timed, then a
     # vector of physical chunks chosen by timing the draw into each competes)
-    out, dinfo = draw_buffer(out, lambda b: K.posterior_sample(
-        b, m1, m2, var_mode=L.VAR_WELFORD, ratio=4.0, seed=7, chain=0, step=0))
+    out, dinfo = draw_buffer(out, lambda b, off=0: K.posterior_sample(
+        b, m1[off:off + b.numel()], m2[off:off + b.numel()], var_mode=L.VAR_WELFORD, ratio=4.0,
+        seed=7, chain=0, step=0))
     timed("posterior_sample", 12, lambda i: K.posterior_sample(
         out, m1, m2, var_mode=L.VAR_WELFORD, ratio=4.0, seed=7, chain=0, step=i))
     if dinfo is not None:

@@ -79,9 +79,11 @@ def test_place_one_vector_is_parked_and_reused(monkeypatch):
     mean = torch.randn(n, device="cuda", generator=g) * 0.02
     m2 = torch.rand(n, device="cuda", generator=g) * 1e-4
 
-    def launcher(b):
-        return lambda: K.posterior_sample(b, mean, m2, var_mode=L.VAR_WELFORD, ratio=4.0,
-                                          seed=3, chain=1, step=2)
+    def launcher(b, off=0):
+        m = b.numel()
+        return lambda: K.posterior_sample(b, mean[off:off + m], m2[off:off + m],
+                                          var_mode=L.VAR_WELFORD, ratio=4.0, seed=3, chain=1,
+                                          step=2)
     key = ("draw_test", n)
     buf, info = P.place_one(n, "cuda", launcher, lambda f: _time_launch(f, "cuda", 3),
                             budget_bytes=1 << 34, pool_key=key)

@@ -85,23 +85,25 @@ def test_draw_buffer_keeps_small_vectors_and_honours_placement_off(monkeypatch):
     assert out is big and ms is None
 
 
-def test_one_candidates_rank_chunks_fastest_first_then_allocation_order():
+def test_one_candidates_rank_chunks_by_position_then_allocation_order():
     """placement.one_candidates (the posterior draw's output, placement.place_one):
-    the per fastest chunks first, then the next windows of the ranking, then
-    the allocation order; each list once, per distinct chunks in range."""
+    position by position the w-th fastest chunk not yet used, then the
+    allocation order; each list once, per distinct chunks in range."""
     ms = [0.30, 0.10, 0.40, 0.12, 0.11, 0.50]
-    c = P.one_candidates(ms, 2)
-    assert c[0] == [1, 4]                       # the two fastest chunks
-    assert c[1] == [4, 3] and c[2] == [3, 0]    # next windows of the ranking
-    assert c[-1] == [0, 1]                      # allocation order last
+    c = P.one_candidates([ms, ms], 2)                    # both positions alike
+    assert c[0] == [1, 4]                                # the two fastest chunks
+    assert c[1] == [4, 3] and c[2] == [3, 0]             # next windows of the ranking
+    assert c[-1] == [0, 1]                               # allocation order last
     assert len(c) == P.ONE_COMPOSITES + 1
     for ids in c:
         assert len(ids) == 2 and len(set(ids)) == 2 and all(0 <= i < len(ms) for i in ids)
-    # allocation order already among the ranked windows: not repeated
-    assert P.one_candidates([0.1, 0.2, 0.3, 0.4], 2) == [[0, 1], [1, 2], [2, 3]]
+    # the chunk fastest at position 1 differs from position 0's
+    p0 = [0.30, 0.10, 0.40, 0.50]
+    p1 = [0.30, 0.50, 0.40, 0.10]
+    assert P.one_candidates([p0, p1], 2)[0] == [1, 3]
     # one chunk per vector, fewer chunks than windows
-    assert P.one_candidates([0.2, 0.1], 1) == [[1], [0]]
-
+    assert P.one_candidates([[0.2, 0.1]], 1) == [[1], [0]]
+    assert P._one_estimate([p0, p1], 2) == pytest.approx(0.2)
 
 
 def test_moment_pair_halves_of_one_allocation(monkeypatch):
@@ -301,7 +303,7 @@ def test_place_one_escalates_until_a_faster_group_shows(fake_chunks):
         return sum(0.29 if c >= 18 else 0.31 for c in ch) / len(ch)
 
     n = 1 << 20
-    buf, info = P.place_one(n, "cuda:0", lambda b: _FakeLaunch({"out": b}), time_launch,
+    buf, info = P.place_one(n, "cuda:0", lambda b, off: _FakeLaunch({"out": b}), time_launch,
                             budget_bytes=1 << 34)
     assert buf is not None and buf.numel() == n
     assert info["chunks_allocated"] == 20 == len(info["chunk_ms"])
@@ -316,7 +318,7 @@ def test_place_one_escalates_until_the_plain_allocation_is_beaten(fake_chunks):
         ch = fake_chunks[f.roles["out"].data_ptr()]
         return sum(0.28 if c >= 24 else (0.30 if c % 2 else 0.31) for c in ch) / len(ch)
 
-    buf, info = P.place_one(1 << 20, "cuda:0", lambda b: _FakeLaunch({"out": b}), time_launch,
+    buf, info = P.place_one(1 << 20, "cuda:0", lambda b, off: _FakeLaunch({"out": b}), time_launch,
                             budget_bytes=1 << 34, beat_ms=0.585)
     assert info["chunks_allocated"] == 28
     assert info["chosen_ms"] == pytest.approx(0.28) and buf is not None
