@@ -527,9 +527,13 @@ def place(n, device, names, launcher, time_launch, budget_bytes, spare=None, sea
         def times0():
             return {j: t for (i, j), t in times.items() if i == 0}
         if search:
-            # the first pool: every ordered pair ("all") or every chunk against chunk 0
-            for i in range(len(ch.views) if pairs == "all" else 1):
-                for j in range(len(ch.views)):
+            # the first pool: every ordered pair ("all") or every chunk against
+            # chunk 0 — among the first 2 x per + spare chunks only (theta /
+            # mom's share; the pool's other chunks hold the other roles while
+            # pairs are timed: Adam's seven roles would make it 306 pairs)
+            p0 = min(len(ch.views), 2 * per + spare)
+            for i in range(p0 if pairs == "all" else 1):
+                for j in range(p0):
                     if i != j:
                         times[(i, j)] = time_launch(launcher(roles_for(i, j), nchunk))
             found = _fast_pairs_found(times, per) if pairs == "all" else _ref_found(times0(), per)

@@ -636,10 +636,11 @@ def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
             assert info["chunks_per_vector"] == per == 1
             # the placed set is theta + grad + mom (a flat-gradient state's
             # gradient is placed too, chosen after the theta / mom pairing)
-            k0 = 3 * per + 2 * per  # the first pool: every ordered pair timed
+            k0 = 3 * per + 2 * per  # the first pool
+            p0 = 2 * per + 2 * per  # ... whose first p0 chunks are timed in every ordered pair
             assert info["chunks_allocated"] >= k0
             # chunks added by the escalation are timed against chunk 0 only
-            assert info["pairs_timed"] == k0 * (k0 - 1) + (info["chunks_allocated"] - k0)
+            assert info["pairs_timed"] == p0 * (p0 - 1) + (info["chunks_allocated"] - k0)
             assert len(info["ref_ms"]) == info["chunks_allocated"] - 1
             assert info["chunks_allocated"] <= P.MAX_CHUNKS
             assert info["grad_timed"] == info["chunks_allocated"] - 2

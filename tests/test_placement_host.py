@@ -351,8 +351,9 @@ def test_place_times_the_gradient_after_the_pair(fake_chunks):
     n = 1 << 20
     vecs, info = P.place(n, "cuda:0", ["theta", "grad", "mom"], lambda roles, m: _FakeLaunch(roles),
                          time_launch, budget_bytes=1 << 34, with_torch=False)
-    k0 = 3 * 2 + 2 * 2
-    assert not any(seen_grad[:k0 * (k0 - 1)])             # pair timings: no placed gradient
+    p0 = 2 * 2 + 2 * 2                                    # the pair-timed share of the first pool
+    assert not any(seen_grad[:p0 * (p0 - 1)])             # pair timings: no placed gradient
+    assert info["pairs_timed"] == p0 * (p0 - 1) + info["chunks_allocated"] - (3 * 2 + 2 * 2)
     assert info["grad_timed"] == info["chunks_allocated"] - 2
     assert sorted(info["grad_chunks"]) == [6, 7]
     assert set(vecs) == {"theta", "grad", "mom"}
