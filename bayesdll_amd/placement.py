@@ -77,11 +77,14 @@ FAST_PAIR = 0.97         # a pair this much faster than the median pair is worth
 # when the first pool shows no fast pair, chunks are added `spare` at a time and
 # each new one is timed against chunk 0 only, until one group is this much
 # faster than chunk 0's own (the best of the three pairing levels, DESIGN.md §4,
+# — one process on one box found a single group over all of 62 chunks, 36 GB,
+# profiles/round3/aux/placement_escalation/box10.jsonl, so the cap is the
+# budget (a quarter of the free memory) more than MAX_CHUNKS —
 # not the middle one: at chunk size the best level times 5-7 % below chunk 0's
 # group, the middle one ~3.5 %, profiles/round3/aux/chunk_matrix/) or the pool
 # holds MAX_CHUNKS / the budget
 FAST_REF = 0.95
-MAX_CHUNKS = int(os.environ.get("BDL_PLACEMENT_MAX_CHUNKS", "64"))
+MAX_CHUNKS = int(os.environ.get("BDL_PLACEMENT_MAX_CHUNKS", "128"))
 # > 1: the fastest RETIME candidates (chunk composites or plain pairings) are
 # timed twice more, interleaved, and the best mean wins (A/B knob)
 RETIME = int(os.environ.get("BDL_PLACEMENT_RETIME", "0"))
