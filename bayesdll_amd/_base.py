@@ -157,9 +157,7 @@ class FusedModelBase(nn.Module):
             from . import kernels as K
             params = list(net.parameters())
             n_all = sum(p.numel() for p in params)
-            from .flat import default_grad_mode
-            launch_cfg = K.autotune_once(n_all, params[0].device, self.tune_method,
-                                         place_grad=default_grad_mode() == "flat") \
+            launch_cfg = K.autotune_once(n_all, params[0].device, self.tune_method) \
                 if params and params[0].is_cuda else None
             self._state = FlatState(net, net0, readout_name=getattr(net, "readout_name", None),
                                     bias=getattr(self, "bias", "informative"),

@@ -103,6 +103,7 @@ EXPORTS = {
     "bdl_vmm_map": (C.c_int, [C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_uint64,
                               C.POINTER(C.c_void_p)]),
     "bdl_vmm_unmap": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "bdl_vmm_arena_info": (C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
 }
 
 _lib = None

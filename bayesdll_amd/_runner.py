@@ -200,18 +200,45 @@ def load_checkpoint(path, device):
         return torch.load(path, map_location=device, weights_only=True)
 
 
+def _sampler_indices(loader):
+    """The sample indices one pass of `loader` scores, as a sorted list —
+    defined only for samplers that visit a fixed set of samples once each:
+    SequentialSampler, RandomSampler without replacement over the whole data
+    set, SubsetRandomSampler (its subset).  Any other sampler (weighted, with
+    replacement, num_samples != len) draws a rank-dependent multiset, which
+    shards cannot partition: ValueError."""
+    from torch.utils.data import RandomSampler, SequentialSampler, SubsetRandomSampler
+    s, n = loader.sampler, len(loader.dataset)
+    if isinstance(s, SequentialSampler):
+        return list(range(n))
+    if isinstance(s, RandomSampler):
+        if s.replacement or s.num_samples != n:
+            raise ValueError("a sharded likelihood pass needs a RandomSampler without replacement "
+                             "over the whole data set (num_samples == len(dataset))")
+        return list(range(n))
+    if isinstance(s, SubsetRandomSampler):
+        return sorted(int(i) for i in s.indices)
+    raise ValueError(f"a sharded likelihood pass cannot partition a {type(s).__name__}: "
+                     "use a sequential, random (no replacement) or subset-random sampler")
+
+
 def shard_loader(loader, r, k):
     """Shard r of k of a training loader for a data-parallel likelihood pass,
-    split by SAMPLE index so that the k shards partition the data set whatever
-    order each rank's loader would draw (the reference's train loader
-    shuffles, datasets.py:45-46, and every chain seeds its own generator):
-      * a torch DataLoader over a map-style data set: a DataLoader over the
-        samples r, r + k, ... (same batch size, collate_fn, workers, pinning;
-        no shuffling — the loss sum does not depend on the order);
+    split by SAMPLE index so that the k shards partition the samples the
+    loader visits whatever order each rank's loader would draw (the
+    reference's train loader shuffles, datasets.py:45-46, and every chain
+    seeds its own generator):
+      * a torch DataLoader over a map-style data set: a DataLoader over every
+        k-th sample (from r) of the sorted index list its sampler visits
+        (_sampler_indices: the whole set, or a SubsetRandomSampler's subset),
+        with the loader's batch size, collate_fn, workers and their settings,
+        pinning and timeout; no shuffling — the loss sum does not depend on
+        the order;
       * a list / tuple of batches (identical on every rank): the batches whose
         index is r mod k;
-    anything else (an iterable data set, a custom batch sampler, drop_last —
-    which drops samples that depend on the shuffle) is refused."""
+    anything else (an iterable data set, a custom batch sampler, a sampler
+    with replacement or weights, drop_last — which drops samples that depend
+    on the shuffle) is refused."""
     if k == 1:
         return loader
     from torch.utils.data import DataLoader, IterableDataset, Subset
@@ -225,9 +252,15 @@ def shard_loader(loader, r, k):
         if loader.drop_last:
             raise ValueError("a sharded likelihood pass cannot reproduce drop_last (which samples "
                              "are dropped depends on each rank's shuffle)")
-        return DataLoader(Subset(ds, range(r, len(ds), k)), batch_size=loader.batch_size,
-                          shuffle=False, num_workers=loader.num_workers,
-                          collate_fn=loader.collate_fn, pin_memory=loader.pin_memory)
+        idx = _sampler_indices(loader)[r::k]
+        kw = dict(batch_size=loader.batch_size, shuffle=False, num_workers=loader.num_workers,
+                  collate_fn=loader.collate_fn, pin_memory=loader.pin_memory,
+                  timeout=loader.timeout, worker_init_fn=loader.worker_init_fn)
+        if loader.num_workers > 0:
+            kw.update(persistent_workers=loader.persistent_workers,
+                      prefetch_factor=loader.prefetch_factor,
+                      multiprocessing_context=loader.multiprocessing_context)
+        return DataLoader(Subset(ds, idx), **kw)
     if isinstance(loader, (list, tuple)):
         return [b for i, b in enumerate(loader) if i % k == r]
     raise ValueError(f"a sharded likelihood pass needs a DataLoader or a list of batches, "

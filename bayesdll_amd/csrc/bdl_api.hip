@@ -35,6 +35,9 @@
 #include "bdl_kernels.hpp"
 #include "bdl_placement.h"
 
+#include <mutex>
+#include <vector>
+
 namespace bdl {
 namespace {
 
@@ -994,13 +997,55 @@ int bdl_chunk_release(uint64_t handle) {
   return BDL_OK;
 }
 
+// Virtual-address arena.  Every mapping takes a fresh sub-range of a large
+// reservation made once (bump pointer, 2 MiB aligned), and no sub-range is
+// ever handed out twice: on this stack an address that has been mapped once
+// keeps translating to its first physical backing after hipMemUnmap (below),
+// and an address reserved with a null hint can be one that torch's allocator
+// used and freed (tools/vmm_alias_repro.cpp, scenario after_hipfree), so only
+// addresses from a range this library reserved up front and never reused are
+// known to be clean.  A new arena is reserved when one runs out.
+constexpr size_t kVmmAlign = (size_t)2 << 20;
+constexpr size_t kArenaBytes = (size_t)4 << 40;  // 4 TiB of address space per arena
+
+struct VmmArena {
+  char* base = nullptr;
+  size_t size = 0, used = 0;
+};
+std::mutex g_arena_mu;
+std::vector<VmmArena> g_arenas;
+size_t g_arena_mapped = 0;  // bytes of sub-ranges handed out so far
+
+static hipError_t arena_take(size_t bytes, void** out) {
+  std::lock_guard<std::mutex> lock(g_arena_mu);
+  const size_t need = (bytes + kVmmAlign - 1) / kVmmAlign * kVmmAlign;
+  if (g_arenas.empty() || g_arenas.back().used + need > g_arenas.back().size) {
+    hipError_t e = hipErrorOutOfMemory;
+    void* base = nullptr;
+    size_t size = std::max(kArenaBytes, need);
+    // a smaller arena if the driver refuses the large one
+    for (; size >= need; size /= 2) {
+      e = hipMemAddressReserve(&base, size, kVmmAlign, nullptr, 0);
+      if (e == hipSuccess) break;
+    }
+    if (e != hipSuccess) return e;
+    g_arenas.push_back(VmmArena{(char*)base, size, 0});
+  }
+  VmmArena& a = g_arenas.back();
+  *out = a.base + a.used;
+  a.used += need;
+  g_arena_mapped += need;
+  return hipSuccess;
+}
+
 int bdl_vmm_map(int32_t device, const uint64_t* handles, int32_t nchunks, uint64_t chunk_bytes,
                 void** va) {
   if (!handles || !va) return fail(BDL_ERR_NULL, "bdl_vmm_map: null argument");
   if (nchunks <= 0 || chunk_bytes == 0) return fail(BDL_ERR_ARG, "bdl_vmm_map: empty range");
+  if (chunk_bytes % kVmmAlign) return fail(BDL_ERR_ARG, "bdl_vmm_map: chunk_bytes not 2 MiB aligned");
   const size_t total = (size_t)nchunks * (size_t)chunk_bytes;
   void* base = nullptr;
-  hipError_t e = hipMemAddressReserve(&base, total, (size_t)2 << 20, nullptr, 0);
+  hipError_t e = arena_take(total, &base);
   if (e != hipSuccess) return hip_fail("bdl_vmm_map: hipMemAddressReserve", e);
   int32_t mapped = 0;
   for (; mapped < nchunks; ++mapped) {
@@ -1024,12 +1069,20 @@ int bdl_vmm_map(int32_t device, const uint64_t* handles, int32_t nchunks, uint64
   const int rc = hip_fail("bdl_vmm_map: hipMemMap/hipMemSetAccess", e);
   for (int32_t i = 0; i < mapped; ++i)
     (void)hipMemUnmap((char*)base + (size_t)i * chunk_bytes, chunk_bytes);
-  // the range stays reserved, as after bdl_vmm_unmap: chunks were mapped into
-  // it, so it must never be handed to other chunks (see below)
+  // the sub-range is never handed out again (the bump pointer moved past it)
   return rc;
 }
 
-// The virtual range stays RESERVED after the unmap, for the life of the
+int bdl_vmm_arena_info(uint64_t* reserved_bytes, uint64_t* mapped_bytes) {
+  std::lock_guard<std::mutex> lock(g_arena_mu);
+  uint64_t r = 0;
+  for (const VmmArena& a : g_arenas) r += a.size;
+  if (reserved_bytes) *reserved_bytes = r;
+  if (mapped_bytes) *mapped_bytes = g_arena_mapped;
+  return BDL_OK;
+}
+
+// The virtual sub-range stays taken after the unmap, for the life of the
 // process.  On this stack a virtual address that has been mapped once keeps
 // translating to its FIRST physical backing after hipMemUnmap: mapping other
 // chunks at that address — after hipMemAddressFree and a new reservation that
@@ -1038,10 +1091,7 @@ int bdl_vmm_map(int32_t device, const uint64_t* handles, int32_t nchunks, uint64
 // device synchronisation around the unmap and whether the range is unmapped
 // whole or chunk by chunk (tools/vmm_alias_repro.cpp, plain HIP, one scenario
 // per process: profiles/round3/vmm/).  Only a never-mapped address is correct,
-// so no range is ever reused for other chunks; the Python side parks whole
-// placed sets (still mapped) for reuse instead of unmapping them
-// (bayesdll_amd/placement.py), which keeps the reserved address space from
-// growing per chain state.
+// so no sub-range of the arena is ever reused for other chunks.
 int bdl_vmm_unmap(void* va, uint64_t total_bytes) {
   if (!va) return fail(BDL_ERR_NULL, "bdl_vmm_unmap: null va");
   const hipError_t e = hipMemUnmap(va, total_bytes);

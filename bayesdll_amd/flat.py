@@ -110,40 +110,32 @@ def _time_launch(launch, device, reps=5):
     return float(np.median([a.elapsed_time(b) for a, b in ev]))
 
 
-PLACEMENT_BPC = {"csghmc": 1, "sgld": 2, "adam": 2}
+PLACEMENT_BPC = {"csghmc": 1, "sgld": 2, "adam": 2}  # workgroups/CU of the placement probe
 
 
-def placed_vectors(n, device, names, method, place_grad=False):
+def placed_vectors(n, device, names, method, park=False):
     """Allocate the chain's swept fp32 vectors (`names` among theta, grad, mom,
     prior, extra state), zeroed.  With `method` (the sampler's kernel family)
-    and vectors of >= PLACEMENT_MIN_ELEMS, they are built from physical chunks
-    with theta and mom paired fast (bayesdll_amd.placement; DESIGN.md §4
-    "Placement"); otherwise, or when the driver refuses chunk mappings, from
-    torch's allocator.  BDL_PLACEMENT: "search" (default), "order" (chunks in
-    allocation order, no pair timing), "0" (torch's allocator).
+    and vectors of >= PLACEMENT_MIN_ELEMS, the read-modify-write vectors are
+    built from physical chunks with theta and mom paired fast
+    (bayesdll_amd.placement's bounded search; DESIGN.md §4 "Placement"); a
+    gradient vector is always a plain torch allocation, like the gradients
+    autograd hands the Runners.  Otherwise, or when the driver refuses chunk
+    mappings, torch's allocator.  BDL_PLACEMENT: "search" (default), "order"
+    (chunks in allocation order, no timing), "0" (torch's allocator).
+    park: the placed set is parked when its vectors die (the autotuner's
+    scratch state, whose set the chain state then takes).
     Returns ({name: tensor}, info or None)."""
-    import os
+    from . import placement as P
     f32 = dict(dtype=torch.float32, device=device)
-    mode = os.environ.get("BDL_PLACEMENT", "search")
-    if mode not in ("search", "order", "0"):
-        raise ValueError(f"BDL_PLACEMENT must be search, order or 0, got {mode!r}")
+    mode = P.mode()
     if method is None or n < PLACEMENT_MIN_ELEMS or "mom" not in names or "theta" not in names \
             or mode == "0":
         return {nm: torch.zeros(n, **f32) for nm in names}, None
-    from . import placement as P
     free, _ = torch.cuda.mem_get_info(device)
     runs_by_n = {}
-    # the gradient is read-only in every sweep; its memory moved the sweep by
-    # 0.3 % on one box (profiles/round2/placement/role_mix/) and ~2 % on
-    # another (tools/grad_spread.py, round 3).  A flat gradient vector the
-    # state keeps (place_grad: "flat" gradient mode) is placed with the set —
-    # chosen after the (theta, mom) pairing; a "tensor"-mode state, whose
-    # gradients are autograd's own, gets a plain scratch vector it drops at
-    # once, outside the set (so the set's key says which kind it is)
-    place_grad = place_grad and "grad" in names and os.environ.get("BDL_PLACEMENT_GRAD", "1") != "0"
-
-    pnames = [nm for nm in names if nm != "grad" or place_grad]
-    grad = torch.zeros(n, **f32) if "grad" in names and not place_grad else None
+    pnames = [nm for nm in names if nm != "grad"]
+    grad = torch.zeros(n, **f32) if "grad" in names else None
     per, cb = P.chunk_geometry(n)
     gsrc = grad if grad is not None and cb // 4 <= n else torch.zeros(max(n, cb // 4), **f32)
 
@@ -156,14 +148,13 @@ def placed_vectors(n, device, names, method, place_grad=False):
     # the probe kernel's depth is fixed at 4; workgroups per CU: the method's
     # usual optimum at that depth (cSGHMC 1, the VALU-heavier SGLD / Adam
     # sweeps 2 — at 1 they are occupancy-bound and placement barely shows),
-    # whatever geometry another state installed; BDL_PLACEMENT_BPC overrides
-    bpc = int(os.environ.get("BDL_PLACEMENT_BPC", "0")) or PLACEMENT_BPC.get(method, 1)
-    prev = K.set_launch_config(bpc, 4, 1)
+    # whatever geometry another state installed
+    prev = K.set_launch_config(PLACEMENT_BPC.get(method, 1), 4, 1)
     try:
         vecs, info = P.place(n, device, pnames, launcher, lambda f: _time_launch(f, device, 5),
                              budget_bytes=int(0.25 * free), search=mode == "search",
-                             pool_key=(method, bpc))
-    except RuntimeError as e:  # chunk mappings unavailable: plain allocations
+                             pool_key=(method,), park=park)
+    except RuntimeError as e:  # chunk mappings unavailable / over budget: plain allocations
         import warnings
         warnings.warn(f"bayesdll_amd: physical-chunk placement unavailable ({e}); "
                       "using torch's allocator")
@@ -183,20 +174,17 @@ def placed_moments(theta, need_m2=True):
     bdl_moments_update sweep (methods/sgld.py:95-102 seeding, :236-246 the
     running mean; theta r, m1 rw, m2 rw), zeroed, placed the way the step's
     theta / mom pair is: that sweep is fast iff its two read-modify-write
-    streams m1 / m2 sit in different physical groups (DESIGN.md §4,
-    profiles/round2/placement/aux_roles/: 0.965-0.973 vs 1.04-1.08 ms for
-    ViT-L/32), so the pair is built from physical chunks whose pairings are
-    timed with the moments kernel itself (bayesdll_amd.placement, roles
-    theta -> m1, mom -> m2; plain torch allocations compete).  Below
-    PLACEMENT_MIN_ELEMS, without m2, or with BDL_PLACEMENT=0: plain
-    allocations.  Values never depend on it.  Returns (m1, m2, info)."""
-    import os
+    streams m1 / m2 sit in different physical groups, so the
+    pair goes through the same bounded search with the moments kernel as the
+    timed launch (roles theta -> m1, mom -> m2).  Below PLACEMENT_MIN_ELEMS,
+    without m2, or with BDL_PLACEMENT=0: plain allocations.  Values never
+    depend on it.  Returns (m1, m2, info)."""
+    from . import placement as P
     n, device = theta.numel(), theta.device
-    mode = os.environ.get("BDL_PLACEMENT", "search")
+    mode = P.mode()
     if not need_m2 or n < PLACEMENT_MIN_ELEMS or mode == "0":
         return (torch.zeros_like(theta), torch.zeros_like(theta) if need_m2 else None, None)
     from . import kernels as K
-    from . import placement as P
 
     def launcher(roles, m):
         k = min(m, n)  # a one-chunk vector's chunk is rounded up past n
@@ -272,8 +260,7 @@ class FlatState:
         # scratch gradient vector, freed after the choice)
         names_ = ["theta", "grad"] + (["mom"] if need_mom else []) + \
             (["prior"] if need_prior else []) + list(extra)
-        vecs, self.placement_info = placed_vectors(self.n, dev, names_, placement,
-                                                   place_grad=self.grad_mode == "flat")
+        vecs, self.placement_info = placed_vectors(self.n, dev, names_, placement)
         if self.grad_mode == "tensor":
             del vecs["grad"]
         # further per-element state of the sampler (e.g. Adam's m, v and the
@@ -333,12 +320,10 @@ class FlatState:
     @classmethod
     def from_segments(cls, segments, readout_name, *, bias="informative", device="cuda",
                       need_prior=False, need_mom=True, need_noise=False, init=None,
-                      placement=None, extra=(), place_grad=True):
+                      placement=None, extra=(), park=False):
         """Flat chain state for a segment table alone (no nn.Module): the
-        benchmark and kernel tests use it with synthetic vectors.
-        place_grad=False: its gradient vector stays outside the placed set (as
-        a "tensor"-gradient-mode chain's scratch, e.g. the autotune scratch of
-        such a chain, whose placed set that chain then takes)."""
+        benchmark and kernel tests use it with synthetic vectors.  park: its
+        placed set is parked when it dies (placement.PlacedSet)."""
         self = cls.__new__(cls)
         self.names = [nm for nm, _ in segments]
         self.shapes = [tuple(s) for _, s in segments]
@@ -357,8 +342,7 @@ class FlatState:
         names_ = (["theta"] if init is None else []) + ["grad"] + (["mom"] if need_mom else []) \
             + (["prior"] if need_prior else []) + list(extra)
         vecs, self.placement_info = placed_vectors(
-            self.n, self.device, names_, placement if init is None else None,
-            place_grad=place_grad)
+            self.n, self.device, names_, placement if init is None else None, park=park)
         self.extra = {nm: vecs[nm].zero_() for nm in extra}
         self.theta = vecs["theta"] if init is None else init
         self.grad_mode = "flat"
@@ -648,47 +632,21 @@ DRAW_CANDIDATES = 3  # output buffers timed for the posterior-draw sweep
 
 
 def draw_buffer(out, launch, candidates=DRAW_CANDIDATES):
-    """Pick the posterior-draw output buffer (DESIGN.md §4 placement: the draw
-    reads m1 / m2 and writes out, and runs 3-4 % faster with out in the
-    physical group opposite to its reads, which only timing reveals).
-    `launch(buf, off=0)` runs the draw into `buf` with its inputs' elements
-    off .. off + buf.numel() (the whole inputs for a full-size buf).  `out` and candidates - 1
-    fresh allocations of its size are each timed (median of 3); then, with
-    BDL_PLACEMENT=search (the default), a vector built from physical chunks
-    chosen by timing the draw into each (placement.place_one, parked and
-    reused by the next draw copy of this size) competes with the fastest of
-    them.  The winner is returned with
-    {"torch_ms": [...], "chunks": place_one's info or None, "kept": "torch" |
-    "chunks"}; losing allocations go back to torch's cache.  Vectors below
-    PLACEMENT_MIN_ELEMS, or BDL_PLACEMENT=0: (`out`, None)."""
-    import os
-    mode = os.environ.get("BDL_PLACEMENT", "search")
-    if out.numel() < PLACEMENT_MIN_ELEMS or mode == "0":
+    """Pick the posterior-draw output buffer: the draw reads m1 / m2 and
+    writes out, and its speed depends on out's physical memory relative to
+    its reads, which only timing reveals.  `launch(buf)` runs
+    the draw into `buf`; `out` and candidates - 1 fresh torch allocations of
+    its size are each timed (median of 3 launches) and the fastest returned
+    with {"torch_ms": [...], "kept": index}; the losers go back to torch's
+    cache.  Vectors below PLACEMENT_MIN_ELEMS, or BDL_PLACEMENT=0: (`out`,
+    None)."""
+    from . import placement as P
+    if out.numel() < PLACEMENT_MIN_ELEMS or P.mode() == "0":
         return out, None
     cands = [out] + [torch.empty_like(out) for _ in range(max(0, candidates - 1))]
     ms = [_time_launch(lambda b=b: launch(b), out.device, 3) for b in cands]
     best = int(np.argmin(ms))
-    info = {"torch_ms": [round(t, 4) for t in ms], "chunks": None, "kept": "torch"}
-    if mode != "search":
-        return cands[best], info
-    from . import placement as P
-    free, _ = torch.cuda.mem_get_info(out.device)
-    try:
-        buf, pinfo = P.place_one(out.numel(), out.device,
-                                 lambda b, off: (lambda: launch(b, off)),
-                                 lambda f: _time_launch(f, out.device, 3),
-                                 budget_bytes=int(0.25 * free), pool_key=("draw",),
-                                 beat_ms=ms[best])
-    except RuntimeError as e:  # chunk mappings unavailable: the plain allocations stand
-        import warnings
-        warnings.warn(f"bayesdll_amd: physical-chunk placement unavailable ({e}); "
-                      "the draw keeps torch's allocation")
-        return cands[best], dict(info, chunks={"error": str(e)[:200]})
-    info["chunks"] = pinfo
-    if buf is None:
-        return cands[best], info
-    info["kept"] = "chunks"
-    return buf, info
+    return cands[best], {"torch_ms": [round(t, 4) for t in ms], "kept": best}
 
 
 MOMENT_PAIR_ALIGN = 64  # elements: m2 starts 256 B after a 256-B boundary
@@ -707,9 +665,9 @@ def moment_pair(n, device):
     below PLACEMENT_MIN_ELEMS, or BDL_PLACEMENT=0: two plain allocations.
     Values never depend on it; torch.save of both halves in one call stores
     the shared storage once."""
-    import os
+    from . import placement as P
     f32 = dict(dtype=torch.float32, device=device)
-    if n < PLACEMENT_MIN_ELEMS or os.environ.get("BDL_PLACEMENT", "search") == "0":
+    if n < PLACEMENT_MIN_ELEMS or P.mode() == "0":
         return torch.empty(n, **f32), torch.empty(n, **f32)
     stride = -(-n // MOMENT_PAIR_ALIGN) * MOMENT_PAIR_ALIGN
     buf = torch.empty(stride + n, **f32)

@@ -329,7 +329,7 @@ def _scratch_launcher(n, dev, method, placed=True):
     return _scratch_launchers(n, dev, method, placed)[0]
 
 
-def _scratch_launchers(n, dev, method, placed=True, place_grad=False):
+def _scratch_launchers(n, dev, method, placed=True):
     """Closures launching `method`'s production kernel over scratch buffers of
     n elements — (plain step, collect step: the same with the posterior-moment
     update; its m1 / m2 are allocated at its first call, for cSGHMC as the
@@ -338,8 +338,7 @@ def _scratch_launchers(n, dev, method, placed=True, place_grad=False):
     (flat.placed_vectors): on plain allocations that happen to pair slowly,
     geometries rank differently than on the placed vectors the sampler then
     sweeps (3 of 38 round-2 bench runs kept a geometry 1.5-3 % slower there
-    than 1 x 4).  place_grad: the gradient vector is placed with the set, as
-    a "flat"-gradient-mode chain's is (the chain then takes this set)."""
+    than 1 x 4)."""
     from .flat import PLACEMENT_MIN_ELEMS, FlatState, moment_pair
     # the same roles as the sampler's own state, so that its placed set, parked
     # when this scratch state dies, is the one the sampler's state then takes
@@ -349,7 +348,7 @@ def _scratch_launchers(n, dev, method, placed=True, place_grad=False):
                                  placement=method if placed and int(n) >= PLACEMENT_MIN_ELEMS
                                  else None,
                                  extra=ADAM_EXTRA if method == "adam" else (),
-                                 place_grad=place_grad)
+                                 park=True)
     st.theta.zero_()
     if method == "csghmc":
         kw = dict(lrs=(1e-4, 1e-4), noise_scale=(0.0, 0.0), noise_mode=L.NOISE_NONE,
@@ -402,7 +401,7 @@ def _device(device):
 
 
 def autotune(n, device=None, reps=6, candidates=None, method="csghmc", placed=True,
-             collect=False, place_grad=False):
+             collect=False):
     """Pick the fastest launch geometry for an n-element sweep on this device.
 
     The update of every element is independent of the launch geometry (noise
@@ -417,7 +416,7 @@ def autotune(n, device=None, reps=6, candidates=None, method="csghmc", placed=Tr
     dev = _device(device)
     if candidates is None:
         candidates = AUTOTUNE_BY_METHOD.get(method, AUTOTUNE_CANDIDATES)
-    launch, launch_collect = _scratch_launchers(n, dev, method, placed, place_grad)
+    launch, launch_collect = _scratch_launchers(n, dev, method, placed)
 
     def pick(fn, cands):
         # round 1: every candidate; round 2: the three fastest again with twice
@@ -479,7 +478,7 @@ def prewarm(n, device=None, method="csghmc", seconds=2.5):
     return k
 
 
-def autotune_once(n, device, method, placed=True, place_grad=False):
+def autotune_once(n, device, method, placed=True):
     """autotune() (plain and collect steps) once per (n, device, method) in this
     process; later calls only re-install the cached winner.  Returns the plain
     step's geometry (collect_config: the collect step's).  BDL_AUTOTUNE=0
@@ -488,8 +487,7 @@ def autotune_once(n, device, method, placed=True, place_grad=False):
         return None
     key = (int(n), str(device), method)
     if key not in _TUNED:
-        best, _, cbest, _ = autotune(n, device, method=method, placed=placed, collect=True,
-                                     place_grad=place_grad)
+        best, _, cbest, _ = autotune(n, device, method=method, placed=placed, collect=True)
         _TUNED[key], _TUNED_COLLECT[key] = best, cbest
     else:
         set_launch_config(*_TUNED[key])

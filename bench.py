@@ -179,6 +179,33 @@ def launch_ranks(n, cmd=None, kill_after=20.0):
     return rc
 
 
+def device_identity(local):
+    """Which physical GPU this rank drives: index, name, PCI address, UUID."""
+    p = torch.cuda.get_device_properties(local)
+    ident = {"device": int(local), "name": p.name,
+             "pci": f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:"
+                    f"{getattr(p, 'pci_device_id', 0):02x}"}
+    uuid = getattr(p, "uuid", None)
+    ident["uuid"] = str(uuid) if uuid is not None else None
+    return ident
+
+
+def check_distinct_devices(idents, backend, device_count, world):
+    """Under RCCL every rank must drive its own GPU: refuse a run on fewer
+    devices than ranks, or with two ranks on one device (the line's n_gpus
+    would be false).  The gloo rehearsal shares devices on purpose.  Returns
+    an error message or None."""
+    if backend == "gloo":
+        return None
+    if device_count < world:
+        return f"{world} ranks but only {device_count} visible GPUs"
+    keys = [(i["pci"], i["uuid"]) for i in idents]
+    if len(set(keys)) != len(keys):
+        dup = sorted({k for k in keys if keys.count(k) > 1})
+        return f"two or more ranks drive the same GPU {dup}"
+    return None
+
+
 def dist_setup(expected):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -190,17 +217,35 @@ def dist_setup(expected):
     if world > 1:
         import torch.distributed as dist
         backend = os.environ.get("BDL_BENCH_BACKEND", "nccl")  # nccl == RCCL on ROCm
+        ndev = torch.cuda.device_count()
         if backend == "gloo":
             # rehearsal of the N-rank path on fewer GPUs (ranks may share a device)
-            local = local % max(1, torch.cuda.device_count())
+            local = local % max(1, ndev)
             torch.cuda.set_device(local)
             dist.init_process_group("gloo")
         else:
+            if local >= ndev:
+                sys.stderr.write(f"bench.py: LOCAL_RANK {local} but only {ndev} visible GPUs\n")
+                sys.exit(3)
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         return dist, rank, world, local
     torch.cuda.set_device(local)
     return None, 0, 1, local
+
+
+def rank_devices(dist, local, world):
+    """Every rank's device identity (all_gather before the timed region); exits
+    with status 3 when the ranks do not drive `world` distinct GPUs under RCCL."""
+    mine = dict(device_identity(local), device_count=torch.cuda.device_count())
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    err = check_distinct_devices(allr, dist.get_backend(), mine["device_count"], world)
+    if err is not None:
+        sys.stderr.write(f"bench.py: {err}\n")
+        dist.destroy_process_group()
+        sys.exit(3)
+    return allr
 
 
 def aux_kernels(st, reps=20):
@@ -237,20 +282,14 @@ def aux_kernels(st, reps=20):
                      "frac": round(gbs / PEAK_HBM_GBS, 4)}
 
     # the output buffer chosen as the Runners' posterior draws choose it
-    # (flat.draw_buffer: the plain allocation and fresh ones timed, then a
-    # vector of physical chunks chosen by timing the draw into each competes)
-    out, dinfo = draw_buffer(out, lambda b, off=0: K.posterior_sample(
-        b, m1[off:off + b.numel()], m2[off:off + b.numel()], var_mode=L.VAR_WELFORD, ratio=4.0,
-        seed=7, chain=0, step=0))
+    # (flat.draw_buffer: the plain allocation and two fresh ones timed)
+    out, dinfo = draw_buffer(out, lambda b: K.posterior_sample(
+        b, m1, m2, var_mode=L.VAR_WELFORD, ratio=4.0, seed=7, chain=0, step=0))
     timed("posterior_sample", 12, lambda i: K.posterior_sample(
         out, m1, m2, var_mode=L.VAR_WELFORD, ratio=4.0, seed=7, chain=0, step=i))
     if dinfo is not None:
         res["posterior_sample"]["out_candidates_ms"] = dinfo["torch_ms"]
         res["posterior_sample"]["out_kept"] = dinfo["kept"]
-        ci = dinfo["chunks"] or {}
-        res["posterior_sample"]["out_chunks"] = {k: ci.get(k) for k in (
-            "chunk_ms", "composites_ms", "chosen_ms", "reused", "seconds", "error", "skipped")
-            if ci.get(k) is not None}
     res["posterior_sample"]["moments"] = "flat.moment_pair"
     del m1, m2, out
     # the running moments of sgld / sghmc (methods/sgld.py:95-102 seeds them
@@ -264,7 +303,7 @@ def aux_kernels(st, reps=20):
     if pinfo is not None:
         res["moments_update"]["placement"] = {k: pinfo.get(k) for k in (
             "allocator", "kept", "seconds", "default_ms", "chosen_ms", "untuned_torch_ms",
-            "composites_ms", "torch_ms", "pairs_timed")}
+            "composites_ms", "pairs_timed", "chunks_allocated", "transient_gb")}
     del s1, s2
     return res
 
@@ -295,6 +334,79 @@ def collect_init_timing(st, m1s, m2s, rank, reps=5):
     gbs = BYTES_PER_ELEM["collect_init"] * st.n / (avg * 1e-3) / 1e9
     return {"avg_ms": round(avg, 4), "bytes_per_elem": BYTES_PER_ELEM["collect_init"],
             "gbs": round(gbs, 1), "frac": round(gbs / PEAK_HBM_GBS, 4), "launches": reps}
+
+
+def event_times(fn, reps, warm=1):
+    """`reps` launches of fn(i), each bracketed by its own HIP events on the
+    launch stream (after `warm` untimed ones); per-launch ms."""
+    for i in range(warm):
+        fn(i)
+    ev = []
+    for i in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn(warm + i)
+        e1.record()
+        ev.append((e0, e1))
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) for a, b in ev]
+
+
+def kind_stats(ms, bytes_per_elem, n):
+    avg = float(np.mean(ms))
+    gbs = bytes_per_elem * n / (avg * 1e-3) / 1e9
+    return {"timed": len(ms), "avg_ms": round(avg, 4),
+            "p10_ms": round(float(np.percentile(ms, 10)), 4),
+            "p50_ms": round(float(np.percentile(ms, 50)), 4),
+            "p90_ms": round(float(np.percentile(ms, 90)), 4),
+            "bytes_per_elem": bytes_per_elem, "gbs": round(gbs, 1),
+            "frac": round(gbs / PEAK_HBM_GBS, 4)}
+
+
+def collect_steady_timing(st, m1s, m2s, spc, rank, reps=12):
+    """Informational, after the timed region: the steady-state Welford collect
+    (methods/csghmc.py:339-345: Philox noise + m1 / M2 update, 36 B/elem) on
+    one of the run's own cycle pairs, `reps` separately bracketed launches
+    (the timed region holds one per thin x 2 steps only)."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    c = max(m1s)
+    lrs = (1e-5, 1e-3)
+    ns = [0.01 * np.sqrt(2 * 0.18 * x) / 1840.0 for x in lrs]
+    cnt0 = spc[c] + 1
+
+    def fn(i):
+        K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_PHILOX,
+                      one_minus_alpha=1 - 0.18, prior_sig=1.0, collect=L.COLLECT_WELFORD,
+                      mom1=m1s[c], mom2=m2s[c], collect_a=float(cnt0 + 2 * i), seed=42 + rank,
+                      chain=rank, step=2_000_000 + i)
+    return kind_stats(event_times(fn, reps), BYTES_PER_ELEM["collect"], st.n)
+
+
+def explore_tensor_grad_timing(st, reps=20):
+    """Informational, after the timed region: the explore step reading the
+    gradient as the Runners read autograd's (default "tensor" gradient mode,
+    methods/csghmc.py:741-778 reads each p.grad): one fresh torch allocation
+    per parameter tensor (296 for ViT-L/32, never placed) through the per-run
+    base table, on the same theta / momentum as the timed region."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    grads = [st.grad[o:o + k].clone() for o, k in zip(st.offsets, st.numels)]
+    flat = st.grad
+    st.use_tensor_grads(grads)
+
+    def fn(i):
+        K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-5, 1e-3), noise_scale=(0.0, 0.0),
+                      noise_mode=L.NOISE_NONE, one_minus_alpha=1 - 0.18, prior_sig=1.0,
+                      seed=0, chain=0, step=3_000_000 + i)
+    try:
+        res = kind_stats(event_times(fn, reps, warm=2), BYTES_PER_ELEM["explore"], st.n)
+    finally:
+        st.grad_mode, st.grad, st.gbase, st._untouched = "flat", flat, None, ()
+        st.runs, st.nruns = st._base_runs
+        del grads
+    res["gradients"] = f"{len(st.numels)} per-tensor torch allocations (unplaced)"
+    return res
 
 
 def cpu_baseline(segs, readout, seconds):
@@ -365,9 +477,12 @@ def e2e_steps(steps, warmup, local, seed, graph=False):
 
 def main():
     a = parse()
+    if not a.placement:  # every vector of the run on torch's allocator (draw and moments too)
+        os.environ["BDL_PLACEMENT"] = "0"
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(a.gpus))
     dist, rank, world, local = dist_setup(a.gpus)
+    devices = rank_devices(dist, local, world) if dist is not None else None
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
     from bayesdll_amd.cyclical import CyclicalSGMCMC
@@ -392,8 +507,7 @@ def main():
         # (its scratch vectors placed like the chain's: their parked set becomes
         # the chain's, bayesdll_amd.placement)
         best, tuned, cbest, ctuned = K.autotune(n_all, device=local, method=tune_method,
-                                                placed=a.placement, collect=True,
-                                                place_grad=a.grad_mode == "flat")
+                                                placed=a.placement, collect=True)
         launch = {"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
                   "autotuned": True,
                   "candidates_ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4) for c, t in tuned.items()},
@@ -409,8 +523,7 @@ def main():
     sgld = a.method == "sgld" or adam  # adam shares config 3's state/driver shape
     st = FlatState.from_segments(segs, readout, device=dev, need_prior=sgld,
                                  placement=tune_method if a.placement else None,
-                                 extra=("adam_m", "adam_v", "sgd_buf") if adam else (),
-                                 place_grad=a.grad_mode == "flat")
+                                 extra=("adam_m", "adam_v", "sgd_buf") if adam else ())
     if launch.get("autotuned"):
         st.launch_cfg, st.collect_cfg = best, cbest
     gen = torch.Generator(device=dev).manual_seed(42 + rank)
@@ -652,6 +765,24 @@ def main():
                                         if traffic is not None else None),
                      "alg_bytes_per_launch": alg_bytes},
     }
+    # after the timed region, on the same state: the steady-state collect over
+    # enough launches for percentiles, and the explore step on per-tensor
+    # gradients (the Runners' default gradient mode)
+    if not sgld and m1s:
+        table["collect_steady"] = dict(collect_steady_timing(st, m1s, m2s, spc, rank),
+                                       launches=0, timed_region=False)
+    if not sgld and a.grad_mode == "flat":
+        ex = explore_tensor_grad_timing(st)
+        ex["vs_flat_explore"] = round(ex["avg_ms"] / table["explore"]["avg_ms"], 4) \
+            if "explore" in table else None
+        table["explore_tensor_grad"] = dict(ex, launches=0, timed_region=False)
+    out["methodology"] = {
+        "timed_kinds": sorted(set(kinds)),
+        "event_stride": timer.stride,
+        "collect_init": "timed after the region (aux_kernels.collect_init): every cycle's Welford "
+                        "pair is initialised before it",
+        "post_region_kinds": [k for k, v in table.items() if v.get("timed_region") is False],
+        "since": "round 3 (rounds 1-2: every launch bracketed, the init collect inside the region)"}
     if dist is not None:
         # every rank's own dominant-kernel time and placement (rank 0's is the
         # roofline above): the slowest GPU sets the aggregate's wall clock
@@ -661,7 +792,11 @@ def main():
         dist.all_gather_object(allr, mine)
         out["per_rank"] = [{"rank": r["rank"], "kernel": r["kernel"], "avg_ms": r["avg_ms"],
                             "frac": round(alg_bytes / (r["avg_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-                            "placement_ms": r["placement_ms"]} for r in allr]
+                            "placement_ms": r["placement_ms"], **devices[i]}
+                           for i, r in enumerate(allr)]
+        out["distributed"] = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                              "device_count": devices[0]["device_count"],
+                              "distinct_devices": len({(d["pci"], d["uuid"]) for d in devices})}
     if not a.no_aux:
         out["aux_kernels"] = aux_kernels(st)
         if not sgld and m1s:

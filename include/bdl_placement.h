@@ -36,7 +36,9 @@ int bdl_chunk_create(int32_t device, uint64_t bytes, uint64_t* handle);
 /* Drop the caller's reference to a chunk (freed when no mapping remains). */
 int bdl_chunk_release(uint64_t handle);
 
-/* Reserve nchunks * chunk_bytes of virtual address space (2 MiB aligned), map
+/* Take nchunks * chunk_bytes (chunk_bytes a multiple of 2 MiB) of virtual
+ * address space from the library's arena — one large reservation made at the
+ * first call, bump-allocated, no sub-range ever handed out twice — map
  * handles[i] at offset i * chunk_bytes, grant `device` read/write; *va
  * receives the base.  A chunk may be mapped at several places. */
 int bdl_vmm_map(int32_t device, const uint64_t* handles, int32_t nchunks, uint64_t chunk_bytes,
@@ -44,10 +46,14 @@ int bdl_vmm_map(int32_t device, const uint64_t* handles, int32_t nchunks, uint64
 
 /* Unmap a range returned by bdl_vmm_map (total = nchunks * chunk_bytes); its
  * physical chunks are freed once unmapped everywhere and released.  The
- * virtual range itself stays reserved for the life of the process: a range
- * handed out again is translated to the old mapping's memory for a while on
- * this driver stack (measured), so ranges are never reused. */
+ * virtual sub-range is never handed out again: on this driver stack an
+ * address mapped once keeps translating to its first backing after the unmap
+ * (measured, tools/vmm_alias_repro.cpp). */
 int bdl_vmm_unmap(void* va, uint64_t total_bytes);
+
+/* Virtual address space the arena holds (*reserved_bytes) and the sub-ranges
+ * handed out so far (*mapped_bytes); either pointer may be null. */
+int bdl_vmm_arena_info(uint64_t* reserved_bytes, uint64_t* mapped_bytes);
 
 #ifdef __cplusplus
 }

@@ -616,10 +616,12 @@ def test_full_size_vit_sghmc_matches_torch():
 
 
 def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
-    """flat.placed_vectors (bayesdll_amd.placement): the vectors are built from
-    physical chunks mapped into one range each, every (theta, mom) chunk
-    pairing is timed, the faster of the chosen / allocation-order assignment
-    is kept, and the update itself never depends on where the vectors live."""
+    """flat.placed_vectors (bayesdll_amd.placement's bounded search): theta and
+    mom are built from physical chunks mapped into one range each, every
+    chunk is timed against chunk 0, the fastest full-size candidate (chunk
+    assignments or plain torch allocations) is kept within the search's
+    bounds, the gradient stays a plain allocation, and the update itself never
+    depends on where the vectors live."""
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
     from bayesdll_amd import placement as P
@@ -634,35 +636,22 @@ def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
             info = st.placement_info
             per, cb = P.chunk_geometry(st.n)
             assert info["chunks_per_vector"] == per == 1
-            # the placed set is theta + grad + mom (a flat-gradient state's
-            # gradient is placed too, chosen after the theta / mom pairing)
-            k0 = 3 * per + 2 * per  # the first pool
-            p0 = 2 * per + 2 * per  # ... whose first p0 chunks are timed in every ordered pair
-            assert info["chunks_allocated"] >= k0
-            # chunks added by the escalation are timed against chunk 0 only
-            assert info["pairs_timed"] == p0 * (p0 - 1) + (info["chunks_allocated"] - k0)
-            assert len(info["ref_ms"]) == info["chunks_allocated"] - 1 - (k0 - p0)
-            assert info["chunks_allocated"] <= P.MAX_CHUNKS
-            assert info["grad_timed"] == info["chunks_allocated"] - 2
-            if info["kept"] != "torch":
-                assert len(info["grad_chunks"]) == per and \
-                    not set(info["grad_chunks"]) & set(info["theta_chunks"] + info["mom_chunks"])
-            nt = 3 + P.TORCH_EXTRA
-            assert len(info["torch_ms"]) == min(P.TORCH_PAIRINGS, nt * (nt - 1) // 2)
-            assert len(info["composites_ms"]) >= 2
-            assert info["chosen_ms"] == min(info["composites_ms"] + info["torch_ms"])
+            assert 2 * per + 2 * per <= info["chunks_allocated"] <= P.MAX_CHUNKS
+            assert info["pairs_timed"] == info["chunks_allocated"] - 1 == len(info["ref_ms"])
+            assert info["chosen_ms"] == min(info["composites_ms"] + [info["untuned_torch_ms"]])
             assert info["chosen_ms"] <= info["default_ms"]
             assert info["allocator"] == ("torch" if info["kept"] == "torch" else "vmm"), info
+            assert info["transient_gb"] <= info["chunks_allocated"] * cb / 2**30 + 3 * 4 * st.n / 2**30
+            assert info["seconds"] < 2.0, info
             if info["kept"] != "torch":
                 assert info["theta_chunks"] != info["mom_chunks"]
+                for v in (st.theta, st.mom):
+                    assert v.data_ptr() % (2 << 20) == 0
             ptrs = {st.theta.data_ptr(), st.grad.data_ptr(), st.mom.data_ptr()}
             assert len(ptrs) == 3
             for v in (st.theta, st.grad, st.mom):
                 assert v.is_cuda and v.numel() == st.n
                 assert not v.any()  # zeroed
-            for v in (st.theta, st.mom):
-                if info["kept"] != "torch":
-                    assert v.data_ptr() % (2 << 20) == 0
         g = torch.Generator(device=DEV).manual_seed(0)
         st.theta.normal_(0, 0.02, generator=g)
         st.grad.normal_(0, 1e-3, generator=g)
@@ -724,11 +713,11 @@ def test_chunk_mapping_lifetime():
 
 
 def test_composites_mapped_one_after_another_do_not_alias():
-    """Placement maps and drops many composites of the same chunks.  A freed
-    virtual range handed out again was translated to the previous mapping's
-    chunks on this stack (tools/vmm_alias_repro.cpp), so bdl_vmm_unmap keeps
-    ranges reserved: every composite must write exactly its own chunks and
-    get a range no earlier mapping had."""
+    """Placement maps and drops many composites of the same chunks.  On this
+    stack an address mapped once keeps translating to its first backing after
+    the unmap (tools/vmm_alias_repro.cpp), so bdl_vmm_map hands out fresh
+    sub-ranges of one arena and never reuses one: every composite must write
+    exactly its own chunks and get an address no earlier mapping had."""
     import random
     from bayesdll_amd import placement as P
     cb = 64 << 20
@@ -737,6 +726,7 @@ def test_composites_mapped_one_after_another_do_not_alias():
     try:
         rng = random.Random(3)
         seen = set()
+        _, mapped0 = P.va_reserved_bytes()
         for _ in range(8):
             ids = rng.sample(range(6), 4)
             a = P.Mapping(0, [ch.handles[k] for k in ids[:2]], cb, 2 * cb // 4).tensor()
@@ -750,24 +740,27 @@ def test_composites_mapped_one_after_another_do_not_alias():
                 v = ch.views[k]
                 assert float(v.min()) == want and float(v.max()) == want, (ids, k)
             del a, b
+        reserved, mapped = P.va_reserved_bytes()
+        assert mapped - mapped0 == 8 * 2 * 2 * cb and reserved >= mapped
     finally:
         ch.release()
 
 
-def test_placed_sets_are_parked_and_reused_without_new_address_space(monkeypatch):
-    """A chain state's placed vectors form a set that is parked, still mapped,
-    when its last tensor dies, and the next state of the same size, roles and
-    method takes it back: same addresses, no new virtual range, no new search,
-    zeroed, and the update gives the same bits (virtual ranges can never be
-    handed to other chunks on this stack: tools/vmm_alias_repro.cpp).  A
-    search for another key unmaps the parked sets first."""
+def test_scratch_sets_are_parked_for_the_chain_and_chain_sets_released(monkeypatch):
+    """The autotuner's scratch state (park=True) parks its placed set when it
+    dies, and the chain state of the same size, roles and method takes it
+    back: same addresses, no new search, zeroed, same bits from the update.
+    A chain state's own set (park=False) is unmapped when its last tensor
+    dies — a parameter view keeps it mapped until then."""
+    import functools
     import gc
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
     from bayesdll_amd import placement as P
     from bayesdll_amd.flat import FlatState, PLACEMENT_MIN_ELEMS
     P.release_pool()
-    monkeypatch.setattr(P, "TORCH_EXTRA", -1)  # chunk composites only: a mapped set to park
+    # chunk composites only, so that there is a mapped set to park
+    monkeypatch.setattr(P, "place", functools.partial(P.place, with_torch=False))
     segs = [("l0.weight", (PLACEMENT_MIN_ELEMS + 5,)), ("fc.weight", (1000,))]
 
     def run(st):
@@ -781,39 +774,31 @@ def test_placed_sets_are_parked_and_reused_without_new_address_space(monkeypatch
         torch.cuda.synchronize()
         return st.theta.clone(), st.mom.clone()
 
-    st = FlatState.from_segments(segs, "fc", device=DEV, placement="csghmc")
-    info0 = st.placement_info
+    scratch = FlatState.from_segments(segs, "fc", device=DEV, placement="csghmc", park=True)
+    info0 = scratch.placement_info
     assert info0["allocator"] == "vmm" and not info0["reused"]
-    ptrs = (st.theta.data_ptr(), st.mom.data_ptr())
-    ref = run(st)
-    va0 = P.va_reserved_bytes()
-    del st
+    ptrs = (scratch.theta.data_ptr(), scratch.mom.data_ptr())
+    ref = run(scratch)
+    del scratch
     gc.collect()
     assert P.pooled_bytes() > 0
-    for _ in range(3):
-        st = FlatState.from_segments(segs, "fc", device=DEV, placement="csghmc")
-        info = st.placement_info
-        assert info["reused"] and info["chosen_ms"] == info0["chosen_ms"]
-        assert (st.theta.data_ptr(), st.mom.data_ptr()) == ptrs
-        assert not st.mom.any()
-        out = run(st)
-        assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1])
-        assert P.va_reserved_bytes() == va0  # no new address space per state
-        del st, out
-        gc.collect()
-    # a parameter view keeps the set alive (not parked) until it goes too
+    _, mapped0 = P.va_reserved_bytes()
     st = FlatState.from_segments(segs, "fc", device=DEV, placement="csghmc")
-    keep = st.theta[:10]
-    del st
+    info = st.placement_info
+    assert info["reused"] and info["chosen_ms"] == info0["chosen_ms"]
+    assert (st.theta.data_ptr(), st.mom.data_ptr()) == ptrs and P.pooled_bytes() == 0
+    assert not st.mom.any() and P.va_reserved_bytes()[1] == mapped0  # no new mapping
+    out = run(st)
+    assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1])
+    keep = st.theta[:10]  # a parameter view keeps the chain's set mapped
+    del st, out
     gc.collect()
-    assert P.pooled_bytes() == 0
+    assert float(keep.sum()) == float(ref[0][:10].sum())
     del keep
     gc.collect()
-    assert P.pooled_bytes() > 0
-    # another key: the parked set is unmapped before its search
-    st2 = FlatState.from_segments(segs[:1], None, device=DEV, placement="csghmc")
-    assert not st2.placement_info["reused"]
-    assert P.pooled_bytes() == 0
+    assert P.pooled_bytes() == 0  # the chain's set was unmapped, not parked
+    st2 = FlatState.from_segments(segs, "fc", device=DEV, placement="csghmc")
+    assert not st2.placement_info["reused"]  # a new search
     del st2
     gc.collect()
     P.release_pool()

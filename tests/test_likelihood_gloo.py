@@ -171,3 +171,34 @@ def test_shard_loader_partitions_samples_and_refuses_what_it_cannot_split():
         shard_loader(torch.utils.data.DataLoader(ds, batch_size=16, drop_last=True), 0, 2)
     with pytest.raises(ValueError, match="DataLoader or a list"):
         shard_loader(iter(_loader()), 0, 2)
+
+
+def test_shard_loader_follows_the_loaders_sampler():
+    """A SubsetRandomSampler's shards partition ITS subset (not the whole data
+    set); samplers that draw a multiset (with replacement, weighted) are
+    refused; worker settings carry over."""
+    from torch.utils.data import (DataLoader, RandomSampler, SubsetRandomSampler,
+                                  WeightedRandomSampler)
+
+    from bayesdll_amd._runner import shard_loader
+    ds = _shuffled_loader(0).dataset
+    subset = list(range(5, len(ds), 3))
+    dl = DataLoader(ds, batch_size=8, sampler=SubsetRandomSampler(subset),
+                    worker_init_fn=print, timeout=0)
+    seen = []
+    for r in range(2):
+        sh = shard_loader(dl, r, 2)
+        assert sh.worker_init_fn is print
+        for x, _ in sh:
+            seen.extend(x[:, 0].tolist())
+    want = [float(ds[i][0][0]) for i in subset]
+    assert sorted(seen) == sorted(want)
+    with pytest.raises(ValueError, match="without replacement"):
+        shard_loader(DataLoader(ds, batch_size=8, sampler=RandomSampler(ds, replacement=True)),
+                     0, 2)
+    with pytest.raises(ValueError, match="num_samples"):
+        shard_loader(DataLoader(ds, batch_size=8, sampler=RandomSampler(ds, num_samples=10)),
+                     0, 2)
+    with pytest.raises(ValueError, match="WeightedRandomSampler"):
+        shard_loader(DataLoader(ds, batch_size=8,
+                                sampler=WeightedRandomSampler([1.0] * len(ds), len(ds))), 0, 2)

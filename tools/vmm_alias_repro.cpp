@@ -18,6 +18,14 @@
 //   late_views       as free_reuse but no views during rounds 1 and 2 (the
 //                    chunks are mapped once each, like an ordinary vector);
 //                    views are created only for the final read
+//   after_hipfree    R1 stays reserved; R2 is reserved at the address of a
+//                    hipMalloc'd block (filled with 7, then hipFree'd) —
+//                    hinted, so the reservation can land there: can memory
+//                    torch's allocator used and freed be mapped safely?
+//   arena            R1 and R2 are consecutive sub-ranges of ONE large
+//                    reservation made at the start, never reused (the
+//                    product's scheme since round 4: bdl_vmm_map bump-allocates
+//                    from an arena)
 //
 // Output: one JSON line (scenario, whether R2 == R1, each chunk's min / max
 // over 257 strided samples, "ok").  Build: hipcc --offload-arch=gfx950 -O2.
@@ -124,8 +132,24 @@ int main(int argc, char** argv) {
       CK(hipMemUnmap(t, g_cb));  // never freed: no recycling from here
     }
   }
-  void* r1 = map_range(&h[0], 2);
+  void* arena = nullptr;
+  if (sc == "arena") CK(hipMemAddressReserve(&arena, 64 * g_cb, 2 << 20, nullptr, 0));
+  void* r1 = nullptr;
+  if (sc == "arena") {
+    r1 = arena;
+    for (int c = 0; c < 2; ++c) CK(hipMemMap((char*)r1 + c * g_cb, g_cb, 0, h[c], 0));
+    set_rw(r1, 2 * g_cb);
+  } else {
+    r1 = map_range(&h[0], 2);
+  }
   fill(r1, 2 * nf, 1.0f);
+  void* freed = nullptr;  // after_hipfree: the address of a freed hipMalloc block
+  if (sc == "after_hipfree") {
+    CK(hipMalloc(&freed, 2 * g_cb));
+    fill(freed, 2 * nf, 7.0f);
+    CK(hipFree(freed));
+    CK(hipDeviceSynchronize());
+  }
 
   void* r2 = nullptr;
   const bool sync = sc == "free_reuse_sync";
@@ -142,6 +166,14 @@ int main(int argc, char** argv) {
     r2 = r1;
   } else if (sc == "fresh_range") {
     r2 = map_range(&h[2], 2);
+  } else if (sc == "arena") {
+    r2 = (char*)arena + 2 * g_cb;  // the next sub-range: never mapped before
+    for (int c = 0; c < 2; ++c) CK(hipMemMap((char*)r2 + c * g_cb, g_cb, 0, h[2 + c], 0));
+    set_rw(r2, 2 * g_cb);
+  } else if (sc == "after_hipfree") {
+    CK(hipMemAddressReserve(&r2, 2 * g_cb, 2 << 20, freed, 0));
+    for (int c = 0; c < 2; ++c) CK(hipMemMap((char*)r2 + c * g_cb, g_cb, 0, h[2 + c], 0));
+    set_rw(r2, 2 * g_cb);
   } else {
     CK(hipMemAddressFree(r1, 2 * g_cb));
     r2 = map_range(&h[2], 2);
@@ -157,9 +189,11 @@ int main(int argc, char** argv) {
     const float want = c < 2 ? 1.0f : 2.0f;
     ok = ok && lo[c] == want && hi[c] == want;
   }
-  std::printf("{\"scenario\":\"%s\",\"chunk_bytes\":%zu,\"r2_is_r1\":%s,\"chunks_minmax\":"
+  std::printf("{\"scenario\":\"%s\",\"chunk_bytes\":%zu,\"r2_is_r1\":%s,"
+              "\"r2_at_freed_hipmalloc\":%s,\"chunks_minmax\":"
               "[[%g,%g],[%g,%g],[%g,%g],[%g,%g]],\"ok\":%s}\n",
-              sc.c_str(), g_cb, r2 == r1 ? "true" : "false", lo[0], hi[0], lo[1], hi[1], lo[2],
+              sc.c_str(), g_cb, r2 == r1 ? "true" : "false",
+              (freed && r2 == freed) ? "true" : "false", lo[0], hi[0], lo[1], hi[1], lo[2],
               hi[2], lo[3], hi[3], ok ? "true" : "false");
   std::fflush(stdout);
   CK(hipDeviceSynchronize());
