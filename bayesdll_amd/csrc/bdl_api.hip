@@ -961,6 +961,9 @@ static hipMemAllocationProp chunk_prop(int32_t device) {
 
 static int hip_fail(const char* what, hipError_t e) {
   g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  // clear the runtime's last error: the caller falls back to torch's
+  // allocator, whose next launch check would otherwise report this failure
+  (void)hipGetLastError();
   return BDL_ERR_LAUNCH;
 }
 
