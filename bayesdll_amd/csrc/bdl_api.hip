@@ -1069,7 +1069,16 @@ int bdl_vmm_map(int32_t device, const uint64_t* handles, int32_t nchunks, uint64
       return BDL_OK;
     }
   }
-  const int rc = hip_fail("bdl_vmm_map: hipMemMap/hipMemSetAccess", e);
+  int rc;
+  {
+    std::lock_guard<std::mutex> lock(g_arena_mu);
+    char where[160];
+    snprintf(where, sizeof where,
+             "bdl_vmm_map: hipMemMap/hipMemSetAccess (arena %zu, offset %.1f of %.1f GiB)",
+             g_arenas.size(), (double)((char*)base - g_arenas.back().base) / 1073741824.0,
+             (double)g_arenas.back().size / 1073741824.0);
+    rc = hip_fail(where, e);
+  }
   for (int32_t i = 0; i < mapped; ++i)
     (void)hipMemUnmap((char*)base + (size_t)i * chunk_bytes, chunk_bytes);
   // the sub-range is never handed out again (the bump pointer moved past it)

@@ -15,7 +15,7 @@ and noise stream).  Two kinds of checks:
   difference forward.  Measured with IDENTICAL code (the oracle loop) on this
   build container's CPU vs the GPU box's CPU: 3e-8 for the first 4 steps, then
   one element jumps to 3.7e-6 and the chain drifts to 6.2e-5 after 16 steps
-  (tools/diag_mlp.py).  The update rule itself is pinned bit-exactly by the
+  (tools/diag_mlp.py, archived: `git show d6fb22c:tools/diag_mlp.py`).  The update rule itself is pinned bit-exactly by the
   prescribed-gradient fixtures (test_gpu_parity.py) and, on a real MLP with
   real autograd, by test_mlp_real_autograd_matches_reference_update_same_gpu
   below (same hardware for both sides -> 1e-5 north-star tolerance).

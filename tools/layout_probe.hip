@@ -123,7 +123,9 @@ void run(const char* name, unsigned rwmask, int trials) {
   int dev = 0, cus = 0;
   CHECK(hipGetDevice(&dev));
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const long tiles[] = {0, 1, 64, 256, 1024};  // float4 groups: separate, 16 B, 1 KiB, 4 KiB, 16 KiB
+  // float4 groups: separate, 16 B, 1 KiB, 4 KiB, 16 KiB (TILES=big: 64 KiB, 1 MiB, 16 MiB, 64 MiB)
+  const long small[] = {0, 1, 64, 256, 1024}, big[] = {0, 1024, 65536, 1048576, 4194304};
+  const long* tiles = getenv("TILES") && !strcmp(getenv("TILES"), "big") ? big : small;
   int nbytes = 0;
   nbytes += RW ? 8 : 0;
   nbytes += NR * 4 + (W ? 4 : 0);
@@ -136,7 +138,8 @@ void run(const char* name, unsigned rwmask, int trials) {
     if (RW) base.ext_rw = alloc(n4);
     for (int r = 0; r < NR; ++r) base.ext_r[r] = alloc(n4);
     if (W) base.ext_w = alloc(n4);
-    for (long tile : tiles) {
+    for (int ti = 0; ti < 5; ++ti) {
+      const long tile = tiles[ti];
       Args a = base;
       a.tile = tile;
       a.nseg = 1;

@@ -57,5 +57,31 @@ int main() {
   }
   printf("{\"all_ok\": true, \"ok_maps\": %zu, \"last_offset_gb\": %.1f}\n", ok,
          off / 1073741824.0);
+  // further reservations of the same size (an arena that ran out is followed
+  // by another): map one chunk at the start, middle and end of each
+  const int extra = getenv("ARENAS") ? atoi(getenv("ARENAS")) - 1 : 3;
+  for (int k = 0; k < extra; ++k) {
+    void* b2 = nullptr;
+    e = hipMemAddressReserve(&b2, arena_gb << 30, 2 << 20, nullptr, 0);
+    printf("{\"arena\": %d, \"reserve\": \"%s\", \"base\": \"%p\"", k + 1, hipGetErrorString(e), b2);
+    if (e != hipSuccess) {
+      printf("}\n");
+      (void)hipGetLastError();
+      break;
+    }
+    const size_t offs[] = {0, (arena_gb << 29), (arena_gb << 30) - chunk};
+    for (size_t o : offs) {
+      char* p = (char*)b2 + (o & ~(size_t)((2 << 20) - 1));
+      e = hipMemMap(p, chunk, 0, h, 0);
+      if (e == hipSuccess) e = hipMemSetAccess(p, chunk, &acc, 1);
+      if (e == hipSuccess) e = hipMemset(p, 1, 4096);
+      if (e == hipSuccess) e = hipDeviceSynchronize();
+      printf(", \"map_at_%.0fgb\": \"%s\"", (p - (char*)b2) / 1073741824.0, hipGetErrorString(e));
+      if (e == hipSuccess) hipMemUnmap(p, chunk);
+      (void)hipGetLastError();
+    }
+    printf("}\n");
+    fflush(stdout);
+  }
   return 0;
 }
