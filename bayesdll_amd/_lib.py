@@ -25,7 +25,7 @@ ATTR_HEAD, ATTR_PRIOR, ATTR_SKIP, ATTR_GUNALIGNED = 0x1, 0x2, 0x4, 0x8
 FLAG_FIRST_STEP, FLAG_RECIP_DIV, FLAG_MOMENTUM, FLAG_GRAD_READY = 0x1, 0x2, 0x4, 0x8
 FLAG_PLACEMENT_PROBE = 0x10
 VAR_GIVEN, VAR_RAW_MOMENTS, VAR_WELFORD = 0, 1, 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _fp = C.c_void_p
 
@@ -64,7 +64,8 @@ class AdamArgs(C.Structure):
                 ("bias_corr2", C.c_float), ("eps", C.c_float), ("two_alpha", C.c_float),
                 ("nd", C.c_float), ("temperature", C.c_float), ("inv_bias_corr1", C.c_float),
                 ("inv_bias_corr2", C.c_float), ("inv_temperature", C.c_float),
-                ("pad2", C.c_float), ("grad_is_mom", C.c_int32), ("pad", C.c_int32)]
+                ("pad2", C.c_float), ("grad_is_mom", C.c_int32), ("tile_log2", C.c_int32),
+                ("tile_streams", C.c_int32), ("tile_mask", C.c_uint32)]
 
 
 class MomentsArgs(C.Structure):
@@ -104,6 +105,8 @@ EXPORTS = {
                               C.POINTER(C.c_void_p)]),
     "bdl_vmm_unmap": (C.c_int, [C.c_void_p, C.c_uint64]),
     "bdl_vmm_arena_info": (C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "bdl_stream_mix": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.POINTER(C.c_void_p),
+                                 C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_void_p]),
 }
 
 _lib = None

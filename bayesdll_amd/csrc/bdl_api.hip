@@ -649,6 +649,81 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   return BDL_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// Bare access mix of a sweep (measurement only, bdl_stream_mix): NR 16-B
+// streams read and NW written per float4 group with no arithmetic beyond a
+// sum, in the step kernels' loop shape (unguarded full iterations with all
+// loads first, one guarded tail iteration) — the HBM ceiling of a kernel's
+// exact access pattern on its exact buffers.  Written values: r0 + 0 * r1 +
+// ... (finite, usually r0).
+// ---------------------------------------------------------------------------
+constexpr int kMixMaxR = 8, kMixMaxW = 6;
+struct MixArgs {
+  const float* r[kMixMaxR];
+  float* w[kMixMaxW];
+  int64_t n;
+};
+
+template <int NR, int NW, int U>
+__global__ __launch_bounds__(kBlock) void bdl_mix_kernel(const MixArgs a) {
+  constexpr int64_t kIter = (int64_t)kBlock * U;
+  const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * kIter;
+  int64_t gb = (int64_t)blockIdx.x * kIter;
+  for (; gb + kIter <= nfull; gb += stride) {
+    f4v x[U][NR];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+#pragma unroll
+      for (int r = 0; r < NR; ++r) x[u][r] = vload(a.r[r] + e);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+      f4v acc = x[u][0];
+#pragma unroll
+      for (int r = 1; r < NR; ++r) acc = acc + x[u][r] * 0.0f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) vstore(a.w[w] + e, acc);
+    }
+  }
+  if (gb < ngroups) {
+    for (int u = 0; u < U; ++u) {
+      const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+      if (gi >= ngroups) break;
+      const int64_t e = gi * 4;
+      f4v acc = ld4(a.r[0], e, a.n);
+      for (int r = 1; r < NR; ++r) acc = acc + ld4(a.r[r], e, a.n) * 0.0f;
+      for (int w = 0; w < NW; ++w) st4(a.w[w], e, a.n, acc);
+    }
+  }
+}
+
+typedef void (*MixKernel)(const MixArgs);
+
+template <int NR, int NW>
+MixKernel pick_mix_u(int unroll) {
+  switch (unroll) {
+    case 1: return bdl_mix_kernel<NR, NW, 1>;
+    case 4: return bdl_mix_kernel<NR, NW, 4>;
+    default: return bdl_mix_kernel<NR, NW, 2>;
+  }
+}
+
+// the mixes of the path's sweeps: draw (2, 1), explore / moments (3, 2),
+// SGLD (4, 2), Welford init (3, 4), Welford collect (5, 4), Adam + SGD (7, 5)
+MixKernel pick_mix(int nr, int nw, int unroll) {
+  if (nr == 2 && nw == 1) return pick_mix_u<2, 1>(unroll);
+  if (nr == 3 && nw == 2) return pick_mix_u<3, 2>(unroll);
+  if (nr == 4 && nw == 2) return pick_mix_u<4, 2>(unroll);
+  if (nr == 3 && nw == 4) return pick_mix_u<3, 4>(unroll);
+  if (nr == 5 && nw == 4) return pick_mix_u<5, 4>(unroll);
+  if (nr == 7 && nw == 5) return pick_mix_u<7, 5>(unroll);
+  return nullptr;
+}
+
 }  // namespace
 }  // namespace bdl
 
@@ -805,6 +880,12 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
     return fail(BDL_ERR_NULL, "bdl_adam_step: mom1 is required to collect");
   if (s->flags & BDL_FLAG_GRAD_READY)
     return fail(BDL_ERR_ARG, "bdl_adam_step: GRAD_READY is not an Adam flag (use bdl_sgmcmc_step)");
+  if (ad->tile_log2 < 0 || ad->tile_log2 > 40 || (ad->tile_log2 > 0 &&
+      (ad->tile_streams < 1 || ad->tile_streams > 4 || (ad->tile_mask & ~0xFu) || !ad->tile_mask)))
+    return fail(BDL_ERR_ARG, "bdl_adam_step: tile_log2 in [0, 40]; when tiled, tile_streams in "
+                "[1, 4] and tile_mask a non-empty subset of 0xF");
+  if (ad->tile_log2 > 0 && __builtin_popcount(ad->tile_mask) > ad->tile_streams)
+    return fail(BDL_ERR_ARG, "bdl_adam_step: tile_mask names more streams than tile_streams");
   const void* ptrs[] = {s->theta, s->mom, s->prior_mean, s->noise, s->mom1, s->mom2,
                         ad->adam_m, ad->adam_v, ad->sgd_buf};
   for (const void* p : ptrs)
@@ -843,6 +924,9 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
   a.adam_m = ad->adam_m;
   a.adam_v = ad->adam_v;
   a.sgd_buf = ad->sgd_buf;
+  a.tiled = ad->tile_log2 > 0 ? (int32_t)ad->tile_mask : 0;
+  a.tshift = ad->tile_log2;
+  a.tstride = ad->tile_log2 > 0 ? ((int64_t)ad->tile_streams << ad->tile_log2) : 0;
   a.b1 = ad->beta1;
   a.omb1 = ad->one_minus_beta1;
   a.b2 = ad->beta2;
@@ -923,6 +1007,43 @@ int bdl_posterior_sample(const bdl_sample_args* s, void* stream) {
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     g_last_error = std::string("bdl_posterior_sample: launch failed: ") + hipGetErrorString(err);
+    return BDL_ERR_LAUNCH;
+  }
+  return BDL_OK;
+}
+
+int bdl_stream_mix(const float* const* reads, int32_t nreads, float* const* writes,
+                   int32_t nwrites, int64_t n, int32_t blocks_per_cu, int32_t unroll,
+                   void* stream) {
+  if (!reads || !writes) return fail(BDL_ERR_NULL, "bdl_stream_mix: null stream list");
+  if (n < 0 || blocks_per_cu < 1 || blocks_per_cu > 16)
+    return fail(BDL_ERR_ARG, "bdl_stream_mix: n >= 0 and blocks_per_cu in [1, 16]");
+  MixKernel k = (nreads <= kMixMaxR && nwrites <= kMixMaxW) ? pick_mix(nreads, nwrites, unroll)
+                                                            : nullptr;
+  if (!k)
+    return fail(BDL_ERR_ARG, "bdl_stream_mix: supported (reads, writes): (2,1) (3,2) (4,2) "
+                "(3,4) (5,4) (7,5)");
+  MixArgs a{};
+  for (int i = 0; i < nreads; ++i) {
+    if (!reads[i] || !aligned16(reads[i]))
+      return fail(BDL_ERR_ALIGN, "bdl_stream_mix: read stream null or not 16-B aligned");
+    a.r[i] = reads[i];
+  }
+  for (int i = 0; i < nwrites; ++i) {
+    if (!writes[i] || !aligned16(writes[i]))
+      return fail(BDL_ERR_ALIGN, "bdl_stream_mix: write stream null or not 16-B aligned");
+    a.w[i] = writes[i];
+  }
+  a.n = n;
+  if (n == 0) return BDL_OK;
+  const int u = unroll == 1 || unroll == 4 ? unroll : 2;
+  const int64_t ngroups = (n + 3) / 4, per = (int64_t)kBlock * u;
+  const int64_t want = (ngroups + per - 1) / per;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)device_cu_count() * blocks_per_cu));
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    g_last_error = std::string("bdl_stream_mix: launch failed: ") + hipGetErrorString(err);
     return BDL_ERR_LAUNCH;
   }
   return BDL_OK;

@@ -186,6 +186,12 @@ struct KArgs {
   float* __restrict__ adam_v;
   float* __restrict__ sgd_buf;
   float b1, omb1, b2, omb2, bc1, bc2, aeps, two_alpha, nd, temp;
+  // Adam state tiling (bdl_adam_args.tile_log2 > 0): the streams of `tiled`
+  // (bit 0 mom, 1 adam_m, 2 adam_v, 3 sgd_buf) are interleaved in one
+  // allocation, 2^tshift float4 groups per stream per tile, tstride groups per
+  // tile of all streams; each pointer is its stream's base in tile 0
+  int32_t tshift, tiled;
+  int64_t tstride;
   // scalar-divisor reciprocals for BDL_FLAG_RECIP_DIV (host-rounded fl32(1/s64))
   float inv_s2, inv_nd, inv_ca, inv_cb, inv_temp, inv_bc1, inv_bc2;
 };
@@ -687,6 +693,25 @@ __device__ __forceinline__ void adam_core(const KArgs& a, const AdamConst& c, fl
   }
 }
 
+// Element offset of float4 group gi in a tiled Adam state stream (e = 4 gi in
+// a separate vector).
+__device__ __forceinline__ int64_t tiled_elem(const KArgs& a, int64_t gi) {
+  const int64_t lo = gi & ((int64_t(1) << a.tshift) - 1);
+  return ((gi >> a.tshift) * a.tstride + lo) * 4;
+}
+
+// Offsets of group gi in (mom, adam_m, adam_v, sgd_buf): tiled or flat.
+struct AdamOff {
+  int64_t vm, m, v, b;
+};
+__device__ __forceinline__ AdamOff adam_offsets(const KArgs& a, int64_t gi) {
+  const int64_t e = gi * 4;
+  if (!a.tiled) return AdamOff{e, e, e, e};
+  const int64_t te = tiled_elem(a, gi);
+  return AdamOff{(a.tiled & 1) ? te : e, (a.tiled & 2) ? te : e, (a.tiled & 4) ? te : e,
+                 (a.tiled & 8) ? te : e};
+}
+
 template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, bool PRIOR, int U>
 __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, int64_t gb,
                                           float eta, float* gp, uint32_t& bad) {
@@ -695,14 +720,16 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
   f4v th[U], g[U], vm[U], m[U], v[U], buf[U], t0[U], ep[U], m1[U], m2[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    const int64_t e = gi * 4;
+    const AdamOff o = adam_offsets(a, gi);
     buf[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
     th[u] = vload(a.theta + e);
     g[u] = vload(gp + e);
-    vm[u] = vload(a.mom + e);
-    m[u] = vload(a.adam_m + e);
-    v[u] = vload(a.adam_v + e);
-    if (!GRADONLY && c.sgd_mom_read) buf[u] = vload(a.sgd_buf + e);
+    vm[u] = vload(a.mom + o.vm);
+    m[u] = vload(a.adam_m + o.m);
+    v[u] = vload(a.adam_v + o.v);
+    if (!GRADONLY && c.sgd_mom_read) buf[u] = vload(a.sgd_buf + o.b);
     if constexpr (PRIOR) t0[u] = vload(a.prior_mean + e);
     if constexpr (NOISE == BDL_NOISE_BUFFER) ep[u] = vload(a.noise + e);
     if constexpr (kReadMoments) {
@@ -734,6 +761,7 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
       m1[u][j] = x1;
       m2[u][j] = x2;
     }
+    const AdamOff o = adam_offsets(a, gi);
     if constexpr (GRADONLY) {
       bad |= nonfinite4(g[u]);
       vstore(gp + e, g[u]);
@@ -741,10 +769,10 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
       bad |= nonfinite4(th[u]);
       vstore(a.theta + e, th[u]);
     }
-    vstore(a.mom + e, vm[u]);
-    vstore(a.adam_m + e, m[u]);
-    vstore(a.adam_v + e, v[u]);
-    if (!GRADONLY && c.sgd_mom) vstore(a.sgd_buf + e, buf[u]);
+    vstore(a.mom + o.vm, vm[u]);
+    vstore(a.adam_m + o.m, m[u]);
+    vstore(a.adam_v + o.v, v[u]);
+    if (!GRADONLY && c.sgd_mom) vstore(a.sgd_buf + o.b, buf[u]);
     if constexpr (COLLECT != BDL_COLLECT_NONE) {
       vstore(a.mom1 + e, m1[u]);
       if (c.has_m2) vstore(a.mom2 + e, m2[u]);
@@ -766,7 +794,14 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
     if (gi >= gend) continue;
     const int64_t e = gi * 4;
     const bool gt = a.gbase != nullptr;  // gradient per tensor (as in chunk_slow)
-    f4v th = ld4(a.theta, e, n), g = gt ? z : ld4(a.grad, e, n), vm = ld4(a.mom, e, n);
+    // tiled streams: the pointer shifted so that index e lands on the group's
+    // tiled slot (ld4 / st4 keep their bound on the flat index)
+    const AdamOff o = adam_offsets(a, gi);
+    float* const pvm = a.mom + (o.vm - e);
+    float* const pm = a.adam_m + (o.m - e);
+    float* const pv = a.adam_v + (o.v - e);
+    float* const pb = a.sgd_buf ? a.sgd_buf + (o.b - e) : nullptr;
+    f4v th = ld4(a.theta, e, n), g = gt ? z : ld4(a.grad, e, n), vm = ld4(pvm, e, n);
     bool gvec = false;
     if (gt) {
       while (rr < a.nruns - 1 && run_end(rr) <= e) ++rr;
@@ -775,9 +810,9 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
         gvec = true;
       }
     }
-    f4v m = ld4(a.adam_m, e, n), v = ld4(a.adam_v, e, n), t0 = ld4(a.prior_mean, e, n);
+    f4v m = ld4(pm, e, n), v = ld4(pv, e, n), t0 = ld4(a.prior_mean, e, n);
     f4v buf = z, ep = z, m1 = z, m2 = z;
-    if (!GRADONLY && c.sgd_mom_read) buf = ld4(a.sgd_buf, e, n);
+    if (!GRADONLY && c.sgd_mom_read) buf = ld4(pb, e, n);
     if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, n);
     if (NOISE == BDL_NOISE_PHILOX) ep = step_noise4(a, gi);
     if (COLLECT == BDL_COLLECT_MEAN) {
@@ -817,10 +852,10 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
       bad |= nonfinite4(th);
       st4(a.theta, e, n, th);
     }
-    st4(a.mom, e, n, vm);
-    st4(a.adam_m, e, n, m);
-    st4(a.adam_v, e, n, v);
-    if (!GRADONLY && c.sgd_mom) st4(a.sgd_buf, e, n, buf);
+    st4(pvm, e, n, vm);
+    st4(pm, e, n, m);
+    st4(pv, e, n, v);
+    if (!GRADONLY && c.sgd_mom) st4(pb, e, n, buf);
     if (COLLECT != BDL_COLLECT_NONE) {
       st4(a.mom1, e, n, m1);
       if (c.has_m2) st4(a.mom2, e, n, m2);

@@ -682,3 +682,65 @@ def fill_normal_per_tensor(vec, numels, generator=None):
         vec[off:off + k].normal_(generator=generator)
         off += k
     return vec
+
+
+TILE_LOG2_MAX = 20  # 2^20 float4 groups = 16 MiB per stream per tile
+
+
+class TiledState:
+    """Per-element sampler state streams (Adam's m, v, SGD buffer, ...)
+    interleaved in ONE allocation: tiles of 2^log2 float4 groups per stream,
+    `len(names)` streams per tile (bdl_adam_args.tile_*, include/bdl_sgmcmc.h).
+    Why: the Adam-SGHMC sweep reads seven and writes five
+    vectors; with the four state vectors as separate allocations its HBM rate
+    depends on where the allocator put them (2.42-2.76 ms for ViT-L/32 over
+    fresh allocations), as one region it does not (2.39-2.40 ms;
+    profiles/round4/layout_big/adam.jsonl, tools/layout_probe.hip).  Values never
+    depend on the layout.
+
+    `stream(name)` is the stream as a torch view: 1-D of n elements when the
+    vector fits one tile, else 2-D [tiles, tile elements] (the last tile's tail
+    past n is padding); `flat(name)` an n-element vector (a copy when 2-D);
+    `load(name, vec)` writes one."""
+
+    def __init__(self, n, names, device, log2=None):
+        self.n, self.names = int(n), tuple(names)
+        groups = max(1, -(-self.n // 4))
+        if log2 is None:
+            log2 = min(TILE_LOG2_MAX, max(0, (groups - 1).bit_length()))
+        self.log2 = max(1, int(log2))  # tile_log2 = 0 means "separate vectors" in the ABI
+        self.tile = 4 << self.log2      # elements per stream per tile
+        self.ntiles = -(-self.n // self.tile)
+        self.block = torch.zeros(self.ntiles * len(self.names) * self.tile, dtype=torch.float32,
+                                 device=device)
+        self._views = {}
+        for s, nm in enumerate(self.names):
+            v = torch.as_strided(self.block, (self.ntiles, self.tile),
+                                 (len(self.names) * self.tile, 1), s * self.tile)
+            self._views[nm] = v[0, :self.n] if self.ntiles == 1 else v
+
+    def stream(self, name):
+        return self._views[name]
+
+    def flat(self, name):
+        v = self._views[name]
+        return v if v.dim() == 1 else v.reshape(-1)[:self.n]
+
+    def load(self, name, vec):
+        v = self._views[name]
+        vec = vec.reshape(-1).to(device=v.device, dtype=torch.float32)
+        if v.dim() == 1:
+            v.copy_(vec)
+        else:
+            full = torch.zeros(self.ntiles * self.tile, dtype=torch.float32, device=v.device)
+            full[:self.n] = vec
+            v.copy_(full.view(self.ntiles, self.tile))
+
+    def abi(self, names):
+        """(tile_log2, tile_streams, tile_mask) for bdl_adam_args: `names` are
+        the kernel's stream slots in mask-bit order (mom, adam_m, adam_v, sgd_buf)."""
+        mask = 0
+        for bit, nm in enumerate(names):
+            if nm in self._views:
+                mask |= 1 << bit
+        return self.log2, len(self.names), mask

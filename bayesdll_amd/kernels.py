@@ -8,6 +8,7 @@ synchronisation happens here.
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 
 import torch
@@ -167,11 +168,13 @@ def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps,
               momentum_decay, nd, temperature=1.0, grad_is_mom=False, lrs, noise_mode,
               sigma2, n_data, mu=0.0, first_step=False, momentum=False, collect=L.COLLECT_NONE,
               mom1=None, mom2=None, collect_a=1.0, collect_b=1.0, seed=0, chain=0, step=0,
-              div_mode=None, noise=None, philox_offset=0):
+              div_mode=None, noise=None, philox_offset=0, tile=None):
     """One fused Adam-preconditioned SGHMC step (methods/adam_sghmc.py:500-553,
     adam_csghmc.py:812-860) + SGD step.  The host-side scalars are formed in
     float64 exactly as the reference's Python does (1 - beta1, 1 - beta1**t,
-    2 * momentum_decay, 1 - momentum_decay); ctypes rounds them to fp32."""
+    2 * momentum_decay, 1 - momentum_decay); ctypes rounds them to fp32.
+    tile: (log2 float4 groups per tile, streams per tile, stream mask) when
+    the state streams live in a TiledState (bdl_adam_args.tile_*), else None."""
     a = _step_args(state, method, lrs=lrs, noise_scale=(0.0, 0.0), noise_mode=noise_mode,
                    one_minus_alpha=1 - momentum_decay, sigma2=sigma2, n_data=n_data, mu=mu,
                    first_step=first_step, momentum=momentum, collect=collect, mom1=mom1,
@@ -192,8 +195,22 @@ def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps,
     ad.inv_bias_corr1, ad.inv_bias_corr2 = _inv(bc1), _inv(bc2)
     ad.inv_temperature = _inv(temperature)
     ad.grad_is_mom = 1 if grad_is_mom else 0
+    if tile is not None:
+        ad.tile_log2, ad.tile_streams, ad.tile_mask = (int(x) for x in tile)
     _launch(state, lambda: L.check(L.lib().bdl_adam_step(a, ad, L.current_stream_handle(state.device)),
                                    "bdl_adam_step"), a, ad)
+
+
+def stream_mix(reads, writes, blocks_per_cu=1, unroll=4):
+    """The bare access mix of a sweep over these buffers (bdl_stream_mix,
+    include/bdl_placement.h): measurement only — the written tensors' contents
+    are destroyed.  Asynchronous, on the current stream."""
+    n = reads[0].numel()
+    dev = reads[0].device
+    rp = (C.c_void_p * len(reads))(*[t.data_ptr() for t in reads])
+    wp = (C.c_void_p * len(writes))(*[t.data_ptr() for t in writes])
+    L.check(L.lib().bdl_stream_mix(rp, len(reads), wp, len(writes), int(n), int(blocks_per_cu),
+                                   int(unroll), L.current_stream_handle(dev)), "bdl_stream_mix")
 
 
 def clip_workspace(state):

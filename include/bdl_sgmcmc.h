@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define BDL_ABI_VERSION 6
+#define BDL_ABI_VERSION 7
 
 typedef enum bdl_status {
   BDL_OK = 0,
@@ -235,7 +235,20 @@ typedef struct bdl_adam_args {
   float inv_temperature;
   float pad2;
   int32_t grad_is_mom;     /* 1: p.grad = v_mom (adam_csghmc); 0: g + v_mom         */
-  int32_t pad;
+  /* State tiling (ABI v7).  tile_log2 = 0: args.mom, adam_m, adam_v and
+   * sgd_buf are separate n-element vectors (the reference's layout).
+   * tile_log2 = L > 0: the streams named by tile_mask (bit 0 args.mom = v_mom,
+   * bit 1 adam_m, bit 2 adam_v, bit 3 sgd_buf) are interleaved in ONE
+   * allocation in tiles of 2^L float4 groups per stream, tile_streams streams
+   * per tile: element e of such a stream lives at
+   *   ptr[((e/4 >> L) * tile_streams * 2^L + (e/4 & (2^L - 1))) * 4 + e % 4]
+   * with ptr the stream's base (block + s * 4 * 2^L floats for stream slot s).
+   * One region instead of four separately allocated ones: on MI355X the
+   * seven-read / five-write sweep then no longer depends on where the
+   * allocator put four vectors. */
+  int32_t tile_log2;
+  int32_t tile_streams;
+  uint32_t tile_mask;
 } bdl_adam_args;
 
 /* Stand-alone posterior-moment update (no parameter update). */
