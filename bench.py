@@ -248,6 +248,28 @@ def rank_devices(dist, local, world):
     return allr
 
 
+MIX_GEOMS = ((1, 4), (2, 4), (2, 2), (3, 4), (4, 2), (1, 1), (2, 1), (4, 1))
+
+
+def mix_ceiling(reads, writes, same, kernel_ms, reps=8):
+    """The HBM ceiling of a kernel's exact access pattern on its exact buffers:
+    the bare mix (bdl_stream_mix — the same streams read and written, no
+    arithmetic, the step kernels' loop shape) at the kernel's own launch
+    geometry and at the best of MIX_GEOMS.  `of_ceiling` = best bare mix time /
+    kernel time.  Destroys the written vectors' contents: run last."""
+    from bayesdll_amd import kernels as K
+
+    def t(bpc, u):
+        return float(np.mean(event_times(lambda i: K.stream_mix(reads, writes, bpc, u), reps,
+                                         warm=2)))
+    same_ms = t(*same)
+    best = min((t(b, u), (b, u)) for b, u in MIX_GEOMS)
+    return {"mix": f"{len(reads)} reads, {len(writes)} writes", "kernel_ms": round(kernel_ms, 4),
+            "same_geometry_ms": round(same_ms, 4), "best_ms": round(best[0], 4),
+            "best_geometry": f"{best[1][0]}wg/cu x{best[1][1]}",
+            "of_ceiling": round(best[0] / kernel_ms, 4)}
+
+
 def aux_kernels(st, reps=20):
     """Informational, after the timed region: the other full-vector sweeps of
     the path at the same size, HIP-event timed on the launch stream —
@@ -291,6 +313,9 @@ def aux_kernels(st, reps=20):
         res["posterior_sample"]["out_candidates_ms"] = dinfo["torch_ms"]
         res["posterior_sample"]["out_kept"] = dinfo["kept"]
     res["posterior_sample"]["moments"] = "flat.moment_pair"
+    # the draw's own launch geometry: 2 workgroups/CU x 4 groups (bdl_api.hip BDL_SAMPLE_*)
+    res["posterior_sample"]["mix_ceiling"] = mix_ceiling(
+        [m1, m2], [out], (2, 4), res["posterior_sample"]["avg_ms"])
     del m1, m2, out
     # the running moments of sgld / sghmc (methods/sgld.py:95-102 seeds them
     # from theta at burn-in), allocated as the sgld Runner allocates them:
@@ -304,6 +329,9 @@ def aux_kernels(st, reps=20):
         res["moments_update"]["placement"] = {k: pinfo.get(k) for k in (
             "allocator", "kept", "seconds", "default_ms", "chosen_ms", "untuned_torch_ms",
             "composites_ms", "pairs_timed", "chunks_allocated", "transient_gb")}
+    cfg = getattr(st, "launch_cfg", None) or (2, 4, 1)
+    res["moments_update"]["mix_ceiling"] = mix_ceiling(
+        [st.theta, s1, s2], [s1, s2], (cfg[0], 4), res["moments_update"]["avg_ms"])
     del s1, s2
     return res
 
@@ -807,6 +835,20 @@ def main():
                 v["traffic"] = tj.get(a.backbone, {}).get(k)
         except Exception:  # noqa: BLE001
             pass
+    # last on this state (it overwrites the vectors): the dominant kernel's
+    # access mix, bare, on the same buffers
+    cfg = st.launch_cfg if launch.get("autotuned") else (max(a.blocks_per_cu, 1),
+                                                        max(a.unroll, 1), 1)
+    tiled = getattr(st, "tiled", None) is not None
+    if not adam:
+        rd = [st.theta, st.grad] + ([st.prior] if sgld else []) + [st.mom]
+        out["roofline"]["mix_ceiling"] = mix_ceiling(rd, [st.theta, st.mom], cfg[:2],
+                                                     dom["avg_ms"])
+    elif not tiled:
+        ex = st.extra
+        out["roofline"]["mix_ceiling"] = mix_ceiling(
+            [st.theta, st.grad, st.prior, st.mom, ex["adam_m"], ex["adam_v"], ex["sgd_buf"]],
+            [st.theta, st.mom, ex["adam_m"], ex["adam_v"], ex["sgd_buf"]], cfg[:2], dom["avg_ms"])
     if world == 1 and a.e2e_steps > 0 and a.backbone == "vit_l_32" and not sgld:
         del st, m1s, m2s
         torch.cuda.empty_cache()

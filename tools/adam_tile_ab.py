@@ -6,7 +6,7 @@ other physical memory); within a trial the layouts alternate for ROUNDS
 rounds, HIP-event mean of 10 launches each, at every geometry in GEOMS.
 Also checks that each tiled layout produces the separate layout's bits.
 
-  python tools/adam_tile_ab.py          (TRIALS=3 ROUNDS=2 GEOMS="1,1;1,4;2,2")
+  python tools/adam_tile_ab.py          (TRIALS=3 ROUNDS=2 GEOMS="1,1;2,1;4,1;2,2;4,2;1,4")
 """
 import json
 import os
@@ -26,7 +26,7 @@ LAYOUTS = {"separate": (), "mvb": ("adam_m", "adam_v", "sgd_buf"),
            "all4": ("mom", "adam_m", "adam_v", "sgd_buf"), "mv": ("adam_m", "adam_v")}
 trials = int(os.environ.get("TRIALS", "3"))
 rounds = int(os.environ.get("ROUNDS", "2"))
-geoms = [tuple(int(x) for x in g.split(",")) for g in os.environ.get("GEOMS", "1,1;1,4;2,2").split(";")]
+geoms = [tuple(int(x) for x in g.split(",")) for g in os.environ.get("GEOMS", "1,1;2,1;4,1;2,2;4,2;1,4").split(";")]
 dev = torch.device("cuda", 0)
 segs, readout = segments("vit_l_32", 1000)
 st = FlatState.from_segments(segs, readout, device=dev, placement=None, need_prior=True,
@@ -107,10 +107,19 @@ for trial in range(trials):
     for bpc, unroll in geoms:
         K.set_launch_config(bpc, unroll, 1)
         res = {lay: [] for lay in LAYOUTS}
+        res["bare_mix_separate"] = []
+        sv = sets["separate"][0]
+        reads = [st.theta, st.grad, st.prior, sv["mom"], sv["adam_m"], sv["adam_v"], sv["sgd_buf"]]
+        writes = [st.theta, sv["mom"], sv["adam_m"], sv["adam_v"], sv["sgd_buf"]]
         for _ in range(rounds):
             for lay, (vecs, tile, _) in sets.items():
                 st.theta.copy_(theta0)
+                for nm in SLOTS:  # the bare mix below overwrites the separate layout's state
+                    vecs[nm].zero_()
                 res[lay].append(round(timeit(launcher(vecs, tile)), 4))
+            # the same access mix with no arithmetic, on the separate layout's buffers
+            res["bare_mix_separate"].append(round(timeit(
+                lambda i: K.stream_mix(reads, writes, bpc, unroll)), 4))
         print(json.dumps({"trial": trial, "geom": f"{bpc}x{unroll}", "ms": res,
                           "frac": {k: round(48 * n / (min(v) * 1e-3) / 8e12, 4)
                                    for k, v in res.items()}}), flush=True)
