@@ -863,6 +863,167 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Software-pipelined Adam sweep (not GRADONLY): the next block iteration's
+// loads are issued before this iteration's arithmetic, so the ~420 VALU
+// instructions per float4 group (IEEE divide / sqrt x2 each, Philox) run while
+// the next seven streams are in flight.  Two register sets take turns (the
+// loop body is written twice with the roles swapped: no copies); an iteration
+// that needs the guarded path drains the pipeline.  Same per-element update as
+// adam_fast / adam_slow, so results are bit-identical.
+// ---------------------------------------------------------------------------
+template <int U>
+struct AdamRegs {
+  f4v th[U], g[U], vm[U], m[U], v[U], buf[U], t0[U], ep[U], m1[U], m2[U];
+};
+
+template <int NOISE, int COLLECT, int U>
+__device__ __forceinline__ void adam_pipe_load(const KArgs& a, const AdamConst& c, int64_t gb,
+                                               const float* gp, bool prior, AdamRegs<U>& R) {
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    const int64_t e = gi * 4;
+    const AdamOff o = adam_offsets(a, gi);
+    R.th[u] = vload(a.theta + e);
+    R.g[u] = vload(gp + e);
+    R.vm[u] = vload(a.mom + o.vm);
+    R.m[u] = vload(a.adam_m + o.m);
+    R.v[u] = vload(a.adam_v + o.v);
+    R.buf[u] = c.sgd_mom_read ? vload(a.sgd_buf + o.b) : z;
+    R.t0[u] = prior ? vload(a.prior_mean + e) : z;
+    R.ep[u] = z;
+    if constexpr (NOISE == BDL_NOISE_BUFFER) R.ep[u] = vload(a.noise + e);
+    R.m1[u] = R.m2[u] = z;
+    if constexpr (COLLECT == BDL_COLLECT_MEAN) {
+      R.m1[u] = vload(a.mom1 + e);
+      if (c.has_m2) R.m2[u] = vload(a.mom2 + e);
+    }
+  }
+}
+
+template <int NOISE, int COLLECT, bool RECIP, bool PRIOR, int U>
+__device__ __forceinline__ void adam_pipe_compute(const KArgs& a, const AdamConst& c, int64_t gb,
+                                                  float eta, float* gp, AdamRegs<U>& R,
+                                                  uint32_t& bad) {
+  StepConst cc;  // collect_core only reads inv_ca / inv_cb
+  cc.inv_ca = c.inv_ca;
+  cc.inv_cb = c.inv_cb;
+  (void)gp;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    const int64_t e = gi * 4;
+    if constexpr (NOISE == BDL_NOISE_PHILOX) R.ep[u] = step_noise4(a, gi);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float xt = R.th[u][j], xg = R.g[u][j], xvm = R.vm[u][j], xm = R.m[u][j], xv = R.v[u][j],
+            xb = R.buf[u][j], x1 = R.m1[u][j], x2 = R.m2[u][j];
+      adam_core<NOISE, RECIP, PRIOR, false>(a, c, eta, xt, xg, xvm, xm, xv, xb, R.t0[u][j],
+                                            R.ep[u][j]);
+      collect_core<COLLECT, RECIP>(a, cc, xt, x1, x2);
+      R.th[u][j] = xt;
+      R.vm[u][j] = xvm;
+      R.m[u][j] = xm;
+      R.v[u][j] = xv;
+      R.buf[u][j] = xb;
+      R.m1[u][j] = x1;
+      R.m2[u][j] = x2;
+    }
+    const AdamOff o = adam_offsets(a, gi);
+    bad |= nonfinite4(R.th[u]);
+    vstore(a.theta + e, R.th[u]);
+    vstore(a.mom + o.vm, R.vm[u]);
+    vstore(a.adam_m + o.m, R.m[u]);
+    vstore(a.adam_v + o.v, R.v[u]);
+    if (c.sgd_mom) vstore(a.sgd_buf + o.b, R.buf[u]);
+    if constexpr (COLLECT != BDL_COLLECT_NONE) {
+      vstore(a.mom1 + e, R.m1[u]);
+      if (c.has_m2) vstore(a.mom2 + e, R.m2[u]);
+    }
+  }
+}
+
+// Cursor of the pipelined sweep: the current block iteration, its run and
+// whether its data already sit in the current register set.
+struct AdamPipeCursor {
+  int64_t gb;
+  int r;
+  uint32_t attr;
+  bool fast, loaded;
+};
+
+template <int U>
+__device__ __forceinline__ bool adam_pipe_fast(const KArgs& a, int64_t gb, int& r,
+                                               uint32_t& attr) {
+  constexpr int64_t kIter = (int64_t)kBlock * U;
+  const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
+  if (gb >= ngroups) return false;
+  while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
+  const int64_t gend = min(gb + kIter, ngroups);
+  attr = run_attr(r);
+  return gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 && !(attr & kNoFastPath);
+}
+
+// One block iteration with X as the current register set and Y as the next;
+// false when the block's span is done.
+template <int NOISE, int COLLECT, bool RECIP, int U>
+__device__ __forceinline__ bool adam_pipe_iter(const KArgs& a, const AdamConst& c,
+                                               AdamPipeCursor& k, AdamRegs<U>& X,
+                                               AdamRegs<U>& Y, uint32_t& bad) {
+  constexpr int64_t kIter = (int64_t)kBlock * U;
+  const int64_t ngroups = (a.n + 3) >> 2;
+  const int64_t gstep = (int64_t)gridDim.x * kIter;
+  if (k.gb >= ngroups) return false;
+  if (!k.fast) {
+    adam_slow<NOISE, COLLECT, RECIP, false, U>(a, c, k.gb, min(k.gb + kIter, ngroups), k.r, bad);
+    k.gb += gstep;
+    k.fast = adam_pipe_fast<U>(a, k.gb, k.r, k.attr);
+    k.loaded = false;
+    return true;
+  }
+  const bool prior = (k.attr & BDL_ATTR_PRIOR) != 0;
+  float* gp = run_grad(a, k.r);
+  if (!k.loaded) adam_pipe_load<NOISE, COLLECT, U>(a, c, k.gb, gp, prior, X);
+  // the next iteration: classify it and issue its loads before this one's math
+  const int64_t nx = k.gb + gstep;
+  int rn = k.r;
+  uint32_t attrn = 0;
+  const bool fastn = adam_pipe_fast<U>(a, nx, rn, attrn);
+  if (fastn)
+    adam_pipe_load<NOISE, COLLECT, U>(a, c, nx, run_grad(a, rn), (attrn & BDL_ATTR_PRIOR) != 0, Y);
+  const float eta = (k.attr & BDL_ATTR_HEAD) ? a.lr1 : a.lr0;
+  if (prior)
+    adam_pipe_compute<NOISE, COLLECT, RECIP, true, U>(a, c, k.gb, eta, gp, X, bad);
+  else
+    adam_pipe_compute<NOISE, COLLECT, RECIP, false, U>(a, c, k.gb, eta, gp, X, bad);
+  k.gb = nx;
+  k.r = rn;
+  k.attr = attrn;
+  k.fast = fastn;
+  k.loaded = fastn;
+  return true;
+}
+
+template <int NOISE, int COLLECT, bool RECIP, int U>
+__device__ __forceinline__ void adam_pipe_sweep(const KArgs& a, const AdamConst& c,
+                                                uint32_t& bad) {
+  constexpr int64_t kIter = (int64_t)kBlock * U;
+  AdamPipeCursor k;
+  k.gb = (int64_t)blockIdx.x * kIter;
+  k.r = find_run_lds(a.nruns, k.gb * 4);
+  k.attr = 0;
+  k.fast = adam_pipe_fast<U>(a, k.gb, k.r, k.attr);
+  k.loaded = false;
+  AdamRegs<U> A, B;
+  for (;;) {
+    if (!adam_pipe_iter<NOISE, COLLECT, RECIP, U>(a, c, k, A, B, bad)) break;
+    if (!adam_pipe_iter<NOISE, COLLECT, RECIP, U>(a, c, k, B, A, bad)) break;
+  }
+}
+
 template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, int U>
 __device__ __forceinline__ void adam_body(const KArgs& a) {
   AdamConst c;
@@ -880,6 +1041,14 @@ __device__ __forceinline__ void adam_body(const KArgs& a) {
   constexpr int64_t kIter = (int64_t)kBlock * U;
   const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
   stage_runs(a);
+#ifdef BDL_ADAM_PIPE
+  if constexpr (!GRADONLY) {
+    uint32_t bad = 0;
+    adam_pipe_sweep<NOISE, COLLECT, RECIP, U>(a, c, bad);
+    report_nonfinite(a, bad);
+    return;
+  }
+#endif
   int r = find_run_lds(a.nruns, (int64_t)blockIdx.x * kIter * 4);
   uint32_t bad = 0;
   for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {

@@ -121,8 +121,8 @@ def placed_vectors(n, device, names, method, park=False):
     (bayesdll_amd.placement's bounded search; DESIGN.md §4 "Placement"); a
     gradient vector is always a plain torch allocation, like the gradients
     autograd hands the Runners.  Otherwise, or when the driver refuses chunk
-    mappings, torch's allocator.  BDL_PLACEMENT: "search" (default), "order"
-    (chunks in allocation order, no timing), "0" (torch's allocator).
+    mappings, torch's allocator.  BDL_PLACEMENT: "0" (torch's allocator, the
+    default), "search", "order" (chunks in allocation order, no timing).
     park: the placed set is parked when its vectors die (the autotuner's
     scratch state, whose set the chain state then takes).
     Returns ({name: tensor}, info or None)."""
@@ -661,13 +661,12 @@ def moment_pair(n, device):
     (profiles/round2/placement/aux_roles/collect_and_sample_by_class.jsonl);
     one allocation puts both halves in one class, and flat.draw_buffer then
     picks an output buffer from the other.  The collect steps that fill them
-    do not care (1.754-1.762 ms over all four class combinations).  Vectors
-    below PLACEMENT_MIN_ELEMS, or BDL_PLACEMENT=0: two plain allocations.
-    Values never depend on it; torch.save of both halves in one call stores
-    the shared storage once."""
-    from . import placement as P
+    do not care (1.754-1.762 ms over all four class combinations).  A layout,
+    not a search: taken whatever BDL_PLACEMENT says.  Vectors below
+    PLACEMENT_MIN_ELEMS: two plain allocations.  Values never depend on it;
+    torch.save of both halves in one call stores the shared storage once."""
     f32 = dict(dtype=torch.float32, device=device)
-    if n < PLACEMENT_MIN_ELEMS or P.mode() == "0":
+    if n < PLACEMENT_MIN_ELEMS:
         return torch.empty(n, **f32), torch.empty(n, **f32)
     stride = -(-n // MOMENT_PAIR_ALIGN) * MOMENT_PAIR_ALIGN
     buf = torch.empty(stride + n, **f32)

@@ -10,8 +10,10 @@ the momentum in one allocation makes every pair slow, tools/layout_probe.hip),
 invisible from user space, and torch's allocator hands out whatever comes
 next.
 
-How — a bounded search, once per chain state (the same default for the
-Runners and bench.py):
+Opt-in (BDL_PLACEMENT=search; the default, for the Runners and bench.py
+alike, is torch's allocator: on the Runner path the search bought no
+end-to-end time and cost 2.2x the transient HBM).  How — a
+bounded search, once per chain state:
 
   1. create physical chunks (hipMemCreate, <= 1 GiB each, `per` per vector),
      each also mapped alone;
@@ -42,8 +44,8 @@ BDL_PLACEMENT_POOL_GB (default POOL_GB_DEFAULT) per process — so the chain
 state that follows takes it back without a second search.  A search for
 another key and `release_pool()` unmap parked sets.
 
-Knobs: BDL_PLACEMENT = search (default) | order (chunks in allocation order,
-no timing) | 0 (torch's allocator); BDL_PLACEMENT_POOL_GB."""
+Knobs: BDL_PLACEMENT = 0 (torch's allocator, the default) | search | order
+(chunks in allocation order, no timing); BDL_PLACEMENT_POOL_GB."""
 from __future__ import annotations
 
 import ctypes as C
@@ -71,7 +73,7 @@ _pending = []  # (device index, va, total bytes) whose unmap was deferred (graph
 
 
 def mode():
-    m = os.environ.get("BDL_PLACEMENT", "search")
+    m = os.environ.get("BDL_PLACEMENT", "0")
     if m not in ("search", "order", "0"):
         raise ValueError(f"BDL_PLACEMENT must be search, order or 0, got {m!r}")
     return m

@@ -67,8 +67,13 @@ def parse():
                     help="skip the posterior-sample / moments sweeps after the timed region")
     ap.add_argument("--prewarm-seconds", type=float, default=0.0,
                     help="untimed back-to-back launches before the measurement (clock ramp)")
-    ap.add_argument("--no-placement", dest="placement", action="store_false",
-                    help="allocate the chain vectors without placement tuning")
+    ap.add_argument("--placement", choices=("0", "search", "order"),
+                    default=os.environ.get("BDL_PLACEMENT", "0"),
+                    help="physical-chunk placement of the chain vectors: 0 = torch's allocator "
+                         "(the default, as for the Runners), search = the opt-in bounded chunk "
+                         "search (bayesdll_amd.placement), order = chunks in allocation order")
+    ap.add_argument("--no-placement", dest="placement", action="store_const", const="0",
+                    help="same as --placement 0")
     ap.add_argument("--event-stride", type=int, default=0,
                     help="bracket every k-th timed launch (and the first of each kind) with "
                          "HIP events; 1 = all, 0 (default) = max(1, min(5, steps // 10)), i.e. "
@@ -505,8 +510,9 @@ def e2e_steps(steps, warmup, local, seed, graph=False):
 
 def main():
     a = parse()
-    if not a.placement:  # every vector of the run on torch's allocator (draw and moments too)
-        os.environ["BDL_PLACEMENT"] = "0"
+    # one setting for every vector of the run (chain state, draw, moments)
+    os.environ["BDL_PLACEMENT"] = a.placement
+    placed = a.placement != "0"
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(a.gpus))
     dist, rank, world, local = dist_setup(a.gpus)
@@ -535,7 +541,7 @@ def main():
         # (its scratch vectors placed like the chain's: their parked set becomes
         # the chain's, bayesdll_amd.placement)
         best, tuned, cbest, ctuned = K.autotune(n_all, device=local, method=tune_method,
-                                                placed=a.placement, collect=True)
+                                                placed=placed, collect=True)
         launch = {"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
                   "autotuned": True,
                   "candidates_ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4) for c, t in tuned.items()},
@@ -550,7 +556,7 @@ def main():
     adam = a.method == "adam_sghmc"
     sgld = a.method == "sgld" or adam  # adam shares config 3's state/driver shape
     st = FlatState.from_segments(segs, readout, device=dev, need_prior=sgld,
-                                 placement=tune_method if a.placement else None,
+                                 placement=tune_method if placed else None,
                                  extra=("adam_m", "adam_v", "sgd_buf") if adam else ())
     if launch.get("autotuned"):
         st.launch_cfg, st.collect_cfg = best, cbest
@@ -775,7 +781,7 @@ def main():
                    "params": n, "tensors": len(segs), "readout": readout,
                    "cycles": a.cycles, "thin": a.thin, "beta": 0.5, "noise": "philox",
                    "parallelism": f"{world} independent chains (1/GPU)",
-                   "grad_mode": a.grad_mode},
+                   "grad_mode": a.grad_mode, "placement": a.placement},
         "hbm_gbs": round(hbm_gbs * world, 1),
         "eval_collective": collective,
         "launch": launch,

@@ -52,16 +52,23 @@ def theta_digest(theta):
 
 class deterministic_autograd:
     """The reference demos' determinism (demo_mnist.py:74 sets
-    cudnn.deterministic) plus the math attention backend: MIOpen's default
-    convolution algorithms and the fused attention kernels' backward can
-    differ run to run, which would hide whether the SAMPLER couples chains.
-    Restores the previous settings on exit (the test process runs others)."""
+    cudnn.deterministic) plus the math attention backend, and MIOpen off for
+    the one convolution (ViT-L/32's 32x32 / stride-32 patch embedding): with
+    cudnn.deterministic MIOpen still picks its solver per process — the lone
+    chain-7 process ran the patch conv as `naive_conv_ab_nonpacked_fwd_nchw` /
+    `_wrw_nchw`, ensemble rank 7 as `Im2d2Col_v2` + Tensile GEMMs
+    (profiles/round4/config5_trace/diff.json, tools/config5_trace.py) — so
+    the gradients' low bits depended on the process, which would hide whether
+    the SAMPLER couples chains.  torch's own convolution (im2col + GEMM) picks
+    its kernels from the shapes alone.  Restores the previous settings on exit
+    (the test process runs others)."""
 
     def __enter__(self):
         b = torch.backends
         self.saved = (b.cudnn.deterministic, b.cudnn.benchmark, b.cuda.flash_sdp_enabled(),
-                      b.cuda.mem_efficient_sdp_enabled())
+                      b.cuda.mem_efficient_sdp_enabled(), b.cudnn.enabled)
         b.cudnn.deterministic, b.cudnn.benchmark = True, False
+        b.cudnn.enabled = False
         b.cuda.enable_flash_sdp(False)
         b.cuda.enable_mem_efficient_sdp(False)
         return self
@@ -71,6 +78,7 @@ class deterministic_autograd:
         b.cudnn.deterministic, b.cudnn.benchmark = self.saved[0], self.saved[1]
         b.cuda.enable_flash_sdp(self.saved[2])
         b.cuda.enable_mem_efficient_sdp(self.saved[3])
+        b.cudnn.enabled = self.saved[4]
 
 
 def run_chain(chain=None):

@@ -25,7 +25,7 @@ def _draws(monkeypatch, placement):
     from bayesdll_amd import _lib as L
     from bayesdll_amd._runner import PosteriorDraw
     if placement:
-        monkeypatch.delenv("BDL_PLACEMENT", raising=False)
+        monkeypatch.setenv("BDL_PLACEMENT", "search")  # opt-in
     else:
         monkeypatch.setenv("BDL_PLACEMENT", "0")
     net = _net()

@@ -615,7 +615,7 @@ def test_full_size_vit_sghmc_matches_torch():
     np.testing.assert_allclose(st.theta.cpu().numpy(), th_ref.cpu().numpy(), rtol=2e-7, atol=1e-12)
 
 
-def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
+def test_placement_tuning_keeps_results_and_picks_the_fastest_set(monkeypatch):
     """flat.placed_vectors (bayesdll_amd.placement's bounded search): theta and
     mom are built from physical chunks mapped into one range each, every
     chunk is timed against chunk 0, the fastest full-size candidate (chunk
@@ -626,6 +626,7 @@ def test_placement_tuning_keeps_results_and_picks_the_fastest_set():
     from bayesdll_amd import kernels as K
     from bayesdll_amd import placement as P
     from bayesdll_amd.flat import FlatState, PLACEMENT_MIN_ELEMS
+    monkeypatch.setenv("BDL_PLACEMENT", "search")  # opt-in
     segs = [("l0.weight", (PLACEMENT_MIN_ELEMS + 3,)), ("fc.weight", (1024,))]
     outs = []
     for placement in (None, "csghmc"):
@@ -747,7 +748,7 @@ def test_composites_mapped_one_after_another_do_not_alias():
 
 
 def test_scratch_sets_are_parked_for_the_chain_and_chain_sets_released(monkeypatch):
-    """The autotuner's scratch state (park=True) parks its placed set when it
+    """(BDL_PLACEMENT=search, opt-in) The autotuner's scratch state (park=True) parks its placed set when it
     dies, and the chain state of the same size, roles and method takes it
     back: same addresses, no new search, zeroed, same bits from the update.
     A chain state's own set (park=False) is unmapped when its last tensor
@@ -760,6 +761,7 @@ def test_scratch_sets_are_parked_for_the_chain_and_chain_sets_released(monkeypat
     from bayesdll_amd.flat import FlatState, PLACEMENT_MIN_ELEMS
     P.release_pool()
     # chunk composites only, so that there is a mapped set to park
+    monkeypatch.setenv("BDL_PLACEMENT", "search")  # opt-in
     monkeypatch.setattr(P, "place", functools.partial(P.place, with_torch=False))
     segs = [("l0.weight", (PLACEMENT_MIN_ELEMS + 5,)), ("fc.weight", (1000,))]
 
@@ -804,13 +806,14 @@ def test_scratch_sets_are_parked_for_the_chain_and_chain_sets_released(monkeypat
     P.release_pool()
 
 
-def test_placed_moments_change_nothing_but_the_addresses():
+def test_placed_moments_change_nothing_but_the_addresses(monkeypatch):
     """flat.placed_moments (the sgld / sghmc running moments, placed for the
     stand-alone moments sweep): same bits as plain allocations through the
     seeding and two running-mean updates (methods/sgld.py:95-102, :236-246)."""
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
     from bayesdll_amd.flat import PLACEMENT_MIN_ELEMS, placed_moments
+    monkeypatch.setenv("BDL_PLACEMENT", "search")  # opt-in
     n = PLACEMENT_MIN_ELEMS + 7
     g = torch.Generator(device=DEV).manual_seed(4)
     thetas = [torch.randn(n, device=DEV, generator=g) for _ in range(3)]
@@ -934,12 +937,13 @@ def test_moment_pair_changes_nothing_but_the_addresses(monkeypatch):
     from bayesdll_amd.flat import FlatState, PLACEMENT_MIN_ELEMS, moment_pair
     segs = [("l0.weight", (PLACEMENT_MIN_ELEMS + 5,)), ("fc.weight", (1027,))]
     res = []
-    for place in ("search", "0"):
-        monkeypatch.setenv("BDL_PLACEMENT", place)
+    for paired in (True, False):
         st = FlatState.from_segments(segs, "fc", device=DEV)
-        m1, m2 = moment_pair(st.n, st.device)
-        paired = m1.untyped_storage().data_ptr() == m2.untyped_storage().data_ptr()
-        assert paired == (place == "search")
+        if paired:
+            m1, m2 = moment_pair(st.n, st.device)
+            assert m1.untyped_storage().data_ptr() == m2.untyped_storage().data_ptr()
+        else:
+            m1, m2 = (torch.empty(st.n, device=st.device) for _ in range(2))
         g = torch.Generator(device=DEV).manual_seed(0)
         st.theta.normal_(0, 0.02, generator=g)
         st.grad.normal_(0, 1e-3, generator=g)

@@ -43,8 +43,8 @@ def test_draw_buffer_keeps_small_vectors_and_honours_placement_off(monkeypatch):
 def test_moment_pair_halves_of_one_allocation(monkeypatch):
     """flat.moment_pair: for vectors of >= PLACEMENT_MIN_ELEMS, m1 / m2 are the
     two halves of one allocation (disjoint, m2 on a 256-B boundary, both
-    contiguous, n elements each); smaller vectors and BDL_PLACEMENT=0 get two
-    plain allocations."""
+    contiguous, n elements each) whatever BDL_PLACEMENT says (a layout, not a
+    search); smaller vectors get two plain allocations."""
     import torch
 
     from bayesdll_amd import flat as F
@@ -61,7 +61,16 @@ def test_moment_pair_halves_of_one_allocation(monkeypatch):
     assert small[0].untyped_storage().data_ptr() != small[1].untyped_storage().data_ptr()
     monkeypatch.setenv("BDL_PLACEMENT", "0")
     a, b = F.moment_pair(F.PLACEMENT_MIN_ELEMS, "cpu")
-    assert a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr()
+    assert a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
+
+
+def test_placement_is_opt_in(monkeypatch):
+    """torch's allocator unless BDL_PLACEMENT asks for the chunk search."""
+    from bayesdll_amd import placement as P
+    monkeypatch.delenv("BDL_PLACEMENT", raising=False)
+    assert P.mode() == "0"
+    monkeypatch.setenv("BDL_PLACEMENT", "search")
+    assert P.mode() == "search"
 
 
 def test_split_groups_needs_two_groups_and_enough_of_each():
