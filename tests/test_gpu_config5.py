@@ -7,15 +7,10 @@ cross-chain posterior-predictive average.
 Checks:
   * every rank samples its own chain (chain id = rank; eight distinct thetas);
   * chain 7 of the ensemble is the chain one process samples alone with chain
-    id 7 (no cross-chain coupling during sampling): theta within the north
-    star's 1e-5 relative, and that difference at least 1000x smaller than the
-    one between chains 6 and 7.  Not bit for bit: the fused update is
-    history-independent, but ViT-L/32's autograd is not across processes on
-    this stack — the ensemble's rank 7 (eight processes sharing the GPU) and
-    the lone process land on two fixed low-bit variants of the gradients
-    (theta bit-sums -...466741 and -...447049 on every box since round 2,
-    INTEGRATION.md §6), and which one a process gets depends on its
-    environment, not on the sampler;
+    id 7 (no cross-chain coupling during sampling): theta bit for bit (the
+    workers run the patch-embedding convolution without MIOpen, whose
+    per-process solver choice gave the two low-bit variants of rounds 2-3,
+    INTEGRATION.md §6), and the distance between chains 6 and 7 nonzero;
   * every rank's predictive is log((1/8) sum_k softmax(s_k)) of the chains' own
     mixture predictives, rebuilt here from each rank's per-chain posterior
     draws (logits_all), and all ranks hold the same one.
@@ -73,9 +68,9 @@ def _run(tmp_path, envs, extra, tag):
 @pytest.mark.timeout(900)
 def test_config5_eight_vit_chains_one_gpu(tmp_path):
     port = _free_port()
-    # chunks in allocation order: eight concurrent placement searches on one GPU
-    # would time each other, and their transient candidate sets add up
-    env0 = dict(os.environ, BDL_PLACEMENT="order")
+    # torch's allocator (the default; eight concurrent placement searches on
+    # one GPU would time each other)
+    env0 = dict(os.environ, BDL_PLACEMENT="0")
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env0.pop(k, None)
     envs = [dict(env0, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(WORLD),
@@ -93,12 +88,13 @@ def test_config5_eight_vit_chains_one_gpu(tmp_path):
     assert len({int(r["theta_bits"]) for r in ranks}) == WORLD  # eight distinct chains
 
     last = ranks[WORLD - 1]
-    np.testing.assert_allclose(single["theta_sub"], last["theta_sub"], rtol=1e-5, atol=1e-7)
-    np.testing.assert_allclose(single["theta_sum"], last["theta_sum"], rtol=1e-5)
+    assert int(single["theta_bits"]) == int(last["theta_bits"])
+    np.testing.assert_array_equal(single["theta_sub"], last["theta_sub"])
+    assert single["theta_sum"] == last["theta_sum"]
     np.testing.assert_allclose(single["logits_all"], last["logits_all"], rtol=1e-5, atol=1e-5)
     same = np.abs(single["theta_sub"].astype(np.float64) - last["theta_sub"]).max()
     other = np.abs(ranks[WORLD - 2]["theta_sub"].astype(np.float64) - last["theta_sub"]).max()
-    assert other > 0 and same * 1000 < other, (same, other)
+    assert other > 0 and same == 0, (same, other)
     print(f"chain 7 alone vs in the ensemble: max |d theta| {same:.3g} "
           f"(bit-sums {int(single['theta_bits'])} / {int(last['theta_bits'])}); "
           f"chain 6 vs 7: {other:.3g}")

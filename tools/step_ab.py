@@ -46,7 +46,7 @@ st.grad.normal_(0.0, 1e-3, generator=gen)
 m1 = st.theta.clone()
 m2 = torch.zeros_like(st.theta)
 n = st.n
-print(json.dumps({"placement": {k: st.placement_info.get(k) for k in
+print(json.dumps({"placement": {k: (st.placement_info or {}).get(k) for k in
                                 ("allocator", "chosen_ms", "untuned_torch_ms", "kept")}}),
       flush=True)
 lrs, alpha, N = (1e-4, 1e-2), 0.18, 1840.0
