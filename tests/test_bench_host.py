@@ -91,3 +91,24 @@ def test_launch_ranks_stops_the_others_and_returns_the_failing_code(tmp_path):
 def test_launch_ranks_kills_ranks_that_ignore_sigterm(tmp_path):
     rc, dt = _launch(tmp_path, 3, fail_rank=0, ignore_term=True, kill_after=1.0)
     assert rc == 7 and dt < 30
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod_ids", BENCH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_distinct_device_check_refuses_shared_or_missing_gpus():
+    """bench.check_distinct_devices: under RCCL every rank must report its own
+    GPU (PCI address + UUID) and the node must show at least N devices; the
+    gloo rehearsal shares one device on purpose."""
+    b = _bench_module()
+    ids = [{"pci": f"0000:{0x10 + r:02x}:00", "uuid": f"GPU-{r}"} for r in range(8)]
+    assert b.check_distinct_devices(ids, "nccl", 8, 8) is None
+    assert "only 4 visible" in b.check_distinct_devices(ids[:8], "nccl", 4, 8)
+    shared = ids[:7] + [dict(ids[3])]
+    assert "same GPU" in b.check_distinct_devices(shared, "nccl", 8, 8)
+    assert b.check_distinct_devices([ids[0]] * 8, "gloo", 1, 8) is None

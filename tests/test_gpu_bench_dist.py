@@ -74,6 +74,12 @@ def test_bench_ranks_gloo(launcher, world):
     assert [r["rank"] for r in pr] == list(range(world))
     assert all(r["kernel"] == d["roofline"]["kernel"] and r["avg_ms"] > 0 and 0 < r["frac"] < 1
                for r in pr)
+    # which physical GPU each rank drove (the gloo rehearsal shares the box's one)
+    assert all(r["pci"] and r["name"] and "uuid" in r and r["device_count"] >= 1 for r in pr)
+    di = d["distributed"]
+    assert di["world_size"] == world and di["backend"] == "gloo"
+    assert di["device_count"] == torch.cuda.device_count()
+    assert di["distinct_devices"] == len({(r["pci"], r["uuid"]) for r in pr}) == 1
 
 
 def test_rccl_process_group_init_as_bench_does():
