@@ -78,7 +78,7 @@ class MomentsArgs(C.Structure):
 class SampleArgs(C.Structure):
     _fields_ = [("out", _fp), ("mom1", _fp), ("mom2", _fp), ("noise", _fp), ("n", C.c_int64),
                 ("var_mode", C.c_int32), ("noise_mode", C.c_int32), ("ratio", C.c_float),
-                ("var_floor", C.c_float), ("inv_ratio", C.c_float), ("pad", C.c_float),
+                ("var_floor", C.c_float), ("inv_ratio", C.c_float), ("blocks_per_cu", C.c_int32),
                 ("seed", C.c_uint64), ("chain", C.c_uint64),
                 ("step", C.c_uint64), ("chain_groups", C.c_uint64)]
 

@@ -523,10 +523,10 @@ int grid_for(int64_t ngroups, int per_block_groups) {
   return (int)std::max<int64_t>(1, std::min(want, cap));
 }
 
-int grid_sample(int64_t ngroups) {
+int grid_sample(int64_t ngroups, int blocks_per_cu) {
   const int64_t per_block = (int64_t)kBlock * BDL_SAMPLE_U;
   const int64_t want = (ngroups + per_block - 1) / per_block;
-  const int64_t cap = (int64_t)device_cu_count() * BDL_SAMPLE_BPC;
+  const int64_t cap = (int64_t)device_cu_count() * (blocks_per_cu > 0 ? blocks_per_cu : BDL_SAMPLE_BPC);
   return (int)std::max<int64_t>(1, std::min(want, cap));
 }
 
@@ -996,13 +996,15 @@ int bdl_posterior_sample(const bdl_sample_args* s, void* stream) {
       (s->chain_groups > 0xFFFFFFFFull || (uint64_t)((s->n + 3) / 4) > 0xFFFFFFFFull))
     return fail(BDL_ERR_ARG, "bdl_posterior_sample: stacked chains need every float4 group "
                 "index below 2^32");
+  if (s->blocks_per_cu < 0 || s->blocks_per_cu > 8)
+    return fail(BDL_ERR_ARG, "bdl_posterior_sample: blocks_per_cu in [0, 8]");
   SArgs a{s->out, s->mom1, s->mom2, s->noise, s->n, s->var_mode, s->noise_mode,
           s->ratio, s->var_floor, s->inv_ratio, s->seed, s->chain, s->step,
           (uint32_t)s->chain_groups};
   const bool floored = s->var_floor >= 0x1p-96f;  // false for NaN
   hipLaunchKernelGGL(pick_sample(s->var_mode, s->mom2 != nullptr, s->inv_ratio != 0.0f,
                                  s->noise_mode, floored),
-                     dim3(grid_sample((s->n + 3) / 4)), dim3(kBlock), 0,
+                     dim3(grid_sample((s->n + 3) / 4, s->blocks_per_cu)), dim3(kBlock), 0,
                      (hipStream_t)stream, a);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) {

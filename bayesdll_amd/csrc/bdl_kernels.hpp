@@ -865,10 +865,15 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
 
 
 // ---------------------------------------------------------------------------
-// Software-pipelined Adam sweep (not GRADONLY): the next block iteration's
-// loads are issued before this iteration's arithmetic, so the ~420 VALU
-// instructions per float4 group (IEEE divide / sqrt x2 each, Philox) run while
-// the next seven streams are in flight.  Two register sets take turns (the
+// Software-pipelined Adam sweep (not GRADONLY; the production path unless
+// built with -DBDL_ADAM_NO_PIPE): the next block iteration's loads are issued
+// before this iteration's arithmetic, so the ~420 VALU instructions per float4
+// group (IEEE divide / sqrt x2 each, Philox) run while the next seven streams
+// are in flight.  One process, same buffers, alternating builds
+// (tools/step_ab.py, profiles/round4/check_b/adam_pipe_ab.jsonl): best
+// geometry 2.406 ms (1 workgroup/CU x 4) vs 2.429 ms unpipelined (4 x 4); at
+// 1 x 4, where one wave per SIMD would otherwise wait out its own arithmetic,
+// 2.406 vs 3.074 ms.  Two register sets take turns (the
 // loop body is written twice with the roles swapped: no copies); an iteration
 // that needs the guarded path drains the pipeline.  Same per-element update as
 // adam_fast / adam_slow, so results are bit-identical.
@@ -1041,8 +1046,8 @@ __device__ __forceinline__ void adam_body(const KArgs& a) {
   constexpr int64_t kIter = (int64_t)kBlock * U;
   const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
   stage_runs(a);
-#ifdef BDL_ADAM_PIPE
-  if constexpr (!GRADONLY) {
+#ifndef BDL_ADAM_NO_PIPE
+  if constexpr (!GRADONLY) {  // production: the software-pipelined sweep
     uint32_t bad = 0;
     adam_pipe_sweep<NOISE, COLLECT, RECIP, U>(a, c, bad);
     report_nonfinite(a, bad);

@@ -253,10 +253,48 @@ def moments_update(theta, mom1, mom2, collect, collect_a=1.0, collect_b=1.0, div
             "bdl_moments_update")
 
 
+SAMPLE_BPC_CANDIDATES = (2, 3, 4)  # workgroups per CU tried for a vector's draw
+SAMPLE_TUNE_MIN = 1 << 24          # smaller draws keep the default (2)
+_SAMPLE_BPC = {}                   # (device index, n) -> workgroups per CU
+
+
+def sample_geometry(n, device):
+    """The posterior draw's tuned workgroups per CU for an n-element vector on
+    `device` (None until posterior_sample tuned it)."""
+    return _SAMPLE_BPC.get((torch.device(device).index, int(n)))
+
+
+def _tune_sample(a, out):
+    """Time the draw at each SAMPLE_BPC_CANDIDATES geometry with its own
+    arguments (each launch writes the same values: same keys), keep the
+    fastest.  Why: the bare access mix of the draw's buffers ranked 3
+    workgroups/CU x 4 ahead of the compiled-in 2 x 4 by 4 % on one box
+    (bench.py aux_kernels.posterior_sample.mix_ceiling), and round 2's probes
+    ranked 2 x 4 first on two others."""
+    stream = L.current_stream_handle(out.device)
+    best = None
+    for bpc in SAMPLE_BPC_CANDIDATES:
+        a.blocks_per_cu = bpc
+        L.check(L.lib().bdl_posterior_sample(a, stream), "bdl_posterior_sample")
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        for _ in range(3):
+            L.check(L.lib().bdl_posterior_sample(a, stream), "bdl_posterior_sample")
+        ev[1].record()
+        ev[1].synchronize()
+        ms = ev[0].elapsed_time(ev[1])
+        if best is None or ms < best[0]:
+            best = (ms, bpc)
+    return best[1]
+
+
 def posterior_sample(out, mom1, mom2, *, var_mode, ratio=1.0, var_floor=1e-12, noise=None,
-                     seed=0, chain=0, step=0, div_mode=None, chain_groups=0):
+                     seed=0, chain=0, step=0, div_mode=None, chain_groups=0, blocks_per_cu=None):
     """out = mom1 + sqrt(clamp(var(mom1, mom2), var_floor)) * eps (eps: buffer or Philox;
-    chain_groups > 0: stacked chains keyed chain + k, bdl_sample_args.chain_groups)."""
+    chain_groups > 0: stacked chains keyed chain + k, bdl_sample_args.chain_groups).
+    blocks_per_cu: the launch's workgroups per CU; None = tuned once per device
+    and size on the first draw of >= SAMPLE_TUNE_MIN elements (outside graph
+    capture), 2 below.  Values never depend on it."""
     L.require_hip(out, "out")
     a = L.SampleArgs()
     a.out, a.mom1 = out.data_ptr(), mom1.data_ptr()
@@ -271,6 +309,13 @@ def posterior_sample(out, mom1, mom2, *, var_mode, ratio=1.0, var_floor=1e-12, n
     a.inv_ratio = _inv(ratio) if _div_flag(div_mode) else 0.0
     a.seed, a.chain, a.step = int(seed), int(chain), int(step) & 0xFFFFFFFFFFFFFFFF
     a.chain_groups = int(chain_groups)
+    if blocks_per_cu is None:
+        key = (out.device.index, int(a.n))
+        blocks_per_cu = _SAMPLE_BPC.get(key, 0)
+        if not blocks_per_cu and a.n >= SAMPLE_TUNE_MIN and \
+                not torch.cuda.is_current_stream_capturing():
+            blocks_per_cu = _SAMPLE_BPC[key] = _tune_sample(a, out)
+    a.blocks_per_cu = int(blocks_per_cu)
     L.check(L.lib().bdl_posterior_sample(a, L.current_stream_handle(out.device)),
             "bdl_posterior_sample")
 

@@ -283,7 +283,7 @@ typedef struct bdl_sample_args {
   float ratio;             /* RAW_MOMENTS multiplier / WELFORD divisor                */
   float var_floor;         /* clamp_(min=...) — 1e-12 in the reference                 */
   float inv_ratio;         /* WELFORD: nonzero -> multiply by it (torch-on-GPU rounding) */
-  float pad;
+  int32_t blocks_per_cu;   /* workgroups per CU, 1-8 (0: 2); the caller may tune it (ABI v7) */
   uint64_t seed, chain, step;
   uint64_t chain_groups;   /* stacked chains, as bdl_step_args.chain_groups (0: one) */
 } bdl_sample_args;

@@ -21,7 +21,7 @@ def _state(n, seed):
     return st, L
 
 
-@pytest.mark.parametrize("method", ["csghmc", "sgld"])
+@pytest.mark.parametrize("method", ["csghmc", "sgld", "adam"])
 def test_results_do_not_depend_on_launch_geometry(method):
     from bayesdll_amd import kernels as K
     n = 3 * (1 << 20) + 13  # ragged: partial float4 group and partial block iterations
@@ -39,6 +39,16 @@ def test_results_do_not_depend_on_launch_geometry(method):
                                   collect=L.COLLECT_WELFORD_INIT if t == 0 else L.COLLECT_WELFORD,
                                   mom1=m1, mom2=m2, collect_a=float(t + 1), seed=3, chain=1,
                                   step=t)
+                elif method == "adam":  # the software-pipelined Adam-SGHMC + SGD sweep
+                    if t == 0:
+                        am, av, ab = (torch.zeros(n, device="cuda") for _ in range(3))
+                    K.adam_step(st, L.ADAM_SGHMC, adam_m=am, adam_v=av, sgd_buf=ab, beta1=0.9,
+                                beta2=0.999, eps=1e-8, t=t + 1, momentum_decay=0.1, nd=1.0,
+                                lrs=(1e-3, 2e-3), noise_mode=L.NOISE_PHILOX, sigma2=1.0,
+                                n_data=100.0, mu=0.5, first_step=t == 0, momentum=True,
+                                collect=L.COLLECT_MEAN if t else L.COLLECT_NONE, mom1=m1,
+                                mom2=m2, collect_a=float(t), collect_b=float(t + 1), seed=3,
+                                chain=1, step=t)
                 else:
                     K.sgmcmc_step(st, L.SGLD, lrs=(1e-3, 2e-3), noise_scale=(1e-2, 2e-2),
                                   noise_mode=L.NOISE_PHILOX, prior_sig=1.0, sigma2=1.0,
@@ -47,7 +57,8 @@ def test_results_do_not_depend_on_launch_geometry(method):
                                   collect_a=float(t + 1), collect_b=float(t + 2), seed=3,
                                   chain=1, step=t)
             torch.cuda.synchronize()
-            outs.append(torch.cat([st.theta, st.mom, m1, m2]).clone())
+            extra = [am, av, ab] if method == "adam" else []
+            outs.append(torch.cat([st.theta, st.mom, m1, m2] + extra).clone())
     finally:
         K.set_launch_config(0, 0, 0)
     for geo, o in zip(GEOMETRIES[1:], outs[1:]):
@@ -67,3 +78,57 @@ def test_state_geometry_is_reinstalled():
         assert prev == (1 << 24) | (3 << 8) | 2  # packed (grid_stride, blocks_per_cu, unroll)
     finally:
         K.set_launch_config(0, 0, 0)
+
+
+@pytest.mark.parametrize("tile_log2", [5, 12])
+def test_adam_tiled_state_equals_separate_vectors(tile_log2):
+    """Adam's m / v / SGD buffer (and v_mom) interleaved in a flat.TiledState
+    (bdl_adam_args.tile_*, ABI v7) give the separate vectors' bits, through the
+    fast and the guarded path (ragged n, run boundaries at the end), with
+    tiles smaller than a block iteration and larger, at two geometries, with
+    Philox noise and running means."""
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.flat import TiledState
+    n = (1 << 20) + 4093
+    slots = ("mom", "adam_m", "adam_v", "sgd_buf")
+    outs = {}
+    try:
+        for layout in ("separate", "tiled3", "tiled4"):
+            for geo in ((1, 4, 1), (2, 2, 1)):
+                st, L = _state(n, 5)
+                K.set_launch_config(*geo)
+                if layout == "separate":
+                    vec = {nm: torch.zeros(n, device="cuda") for nm in slots}
+                    tile, ts = None, None
+                else:
+                    names = slots[1:] if layout == "tiled3" else slots
+                    ts = TiledState(n, names, "cuda", log2=tile_log2)
+                    vec = {nm: ts.stream(nm) if nm in names else torch.zeros(n, device="cuda")
+                           for nm in slots}
+                    tile = ts.abi(slots)
+                if ts is not None and "mom" in ts.names:
+                    ts.load("mom", st.mom)
+                else:
+                    vec["mom"].copy_(st.mom)
+                m1 = torch.zeros(n, device="cuda")
+                m2 = torch.zeros(n, device="cuda")
+                mom0 = st.mom
+                st.mom = vec["mom"]
+                for t in range(3):
+                    K.adam_step(st, L.ADAM_SGHMC, adam_m=vec["adam_m"], adam_v=vec["adam_v"],
+                                sgd_buf=vec["sgd_buf"], beta1=0.9, beta2=0.999, eps=1e-8,
+                                t=t + 1, momentum_decay=0.1, nd=1.0, lrs=(1e-3, 2e-3),
+                                noise_mode=L.NOISE_PHILOX, sigma2=1.0, n_data=100.0, mu=0.5,
+                                first_step=t == 0, momentum=True,
+                                collect=L.COLLECT_MEAN if t else L.COLLECT_NONE, mom1=m1,
+                                mom2=m2, collect_a=float(t), collect_b=float(t + 1), seed=3,
+                                chain=1, step=t, tile=tile)
+                st.mom = mom0
+                torch.cuda.synchronize()
+                flat = [v if v.dim() == 1 else v.reshape(-1)[:n] for v in vec.values()]
+                outs[(layout, geo)] = torch.cat([st.theta, m1, m2] + flat).clone()
+    finally:
+        K.set_launch_config(0, 0, 0)
+    ref = outs[("separate", (1, 4, 1))]
+    for k, o in outs.items():
+        assert torch.equal(o, ref), k

@@ -959,3 +959,51 @@ def test_moment_pair_changes_nothing_but_the_addresses(monkeypatch):
         del st, m1, m2, out
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_posterior_draw_geometry_changes_nothing_and_is_tuned_once():
+    """bdl_sample_args.blocks_per_cu (ABI v7): every geometry draws the same
+    bits; kernels.posterior_sample tunes it once per device and size for
+    vectors of >= SAMPLE_TUNE_MIN elements and reuses the choice."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    n = K.SAMPLE_TUNE_MIN + 4093
+    g = torch.Generator(device=DEV).manual_seed(2)
+    m1 = torch.randn(n, device=DEV, generator=g) * 0.02
+    m2 = torch.rand(n, device=DEV, generator=g) * 1e-4
+    outs = []
+    for bpc in (1, 2, 3, 4, 8):
+        out = torch.empty(n, device=DEV)
+        K.posterior_sample(out, m1, m2, var_mode=L.VAR_WELFORD, ratio=3.0, seed=5, chain=2,
+                           step=7, blocks_per_cu=bpc)
+        outs.append(out)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    K._SAMPLE_BPC.pop((torch.device(DEV).index or 0, n), None)
+    out = torch.empty(n, device=DEV)
+    K.posterior_sample(out, m1, m2, var_mode=L.VAR_WELFORD, ratio=3.0, seed=5, chain=2, step=7)
+    torch.cuda.synchronize()
+    assert K.sample_geometry(n, out.device) in K.SAMPLE_BPC_CANDIDATES
+    assert torch.equal(out, outs[0])
+    with pytest.raises(RuntimeError, match="blocks_per_cu"):
+        K.posterior_sample(out, m1, m2, var_mode=L.VAR_WELFORD, ratio=3.0, blocks_per_cu=9)
+
+
+@pytest.mark.parametrize("nr,nw", [(2, 1), (3, 2), (4, 2), (3, 4), (5, 4), (7, 5)])
+def test_stream_mix_writes_the_first_read_stream(nr, nw):
+    """bdl_stream_mix (the bench's bare access-mix ceiling): every written
+    vector receives reads[0] (+ 0 x the others), at a ragged size and three
+    geometries; unsupported mixes are refused."""
+    from bayesdll_amd import kernels as K
+    n = 3 * (1 << 18) + 5
+    g = torch.Generator(device=DEV).manual_seed(nr * 10 + nw)
+    reads = [torch.randn(n, device=DEV, generator=g) for _ in range(nr)]
+    for bpc, u in ((1, 4), (2, 2), (3, 1)):
+        writes = [torch.full((n,), 7.0, device=DEV) for _ in range(nw)]
+        K.stream_mix(reads, writes, bpc, u)
+        torch.cuda.synchronize()
+        for w in writes:
+            assert torch.equal(w, reads[0])
+    with pytest.raises(RuntimeError, match="supported"):
+        K.stream_mix(reads[:1] * 6, [reads[0]], 1, 4)
