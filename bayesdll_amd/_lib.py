@@ -80,7 +80,8 @@ class SampleArgs(C.Structure):
                 ("var_mode", C.c_int32), ("noise_mode", C.c_int32), ("ratio", C.c_float),
                 ("var_floor", C.c_float), ("inv_ratio", C.c_float), ("blocks_per_cu", C.c_int32),
                 ("seed", C.c_uint64), ("chain", C.c_uint64),
-                ("step", C.c_uint64), ("chain_groups", C.c_uint64)]
+                ("step", C.c_uint64), ("chain_groups", C.c_uint64), ("unroll", C.c_int32),
+                ("pad", C.c_int32)]
 
 
 EXPORTS = {

@@ -433,21 +433,19 @@ __global__ __launch_bounds__(kBlock) void bdl_sample_kernel(const SArgs a) {
 
 typedef void (*SampleKernel)(const SArgs);
 
-// Posterior-sample geometry, independent of the step kernels' tuning: 2
-// workgroups per CU, 4 float4 groups per lane in flight — the best or within
-// 1 % of it on two boxes among {1,2,4} groups x {2,3,4} workgroups/CU for the
-// split loop (tools/sample_probe.hip, profiles/round2/aux/sample_probe*.jsonl;
-// the per-group-guarded loop of round 1 was best at 3).
-#ifndef BDL_SAMPLE_U
-#define BDL_SAMPLE_U 4
-#endif
+// Posterior-sample geometry, independent of the step kernels' tuning:
+// workgroups per CU (bdl_sample_args.blocks_per_cu, default 2) and float4
+// groups per lane in flight (bdl_sample_args.unroll: 4, the default, or 1).
+// The host tunes both once per vector size (kernels.posterior_sample): the
+// bare access mix of the draw's buffers ranked 3 x 4 first at ViT-L/32 size
+// and 4 x 1 at ResNet-101 size on one box (bench.py mix_ceiling), round 2's
+// probes 2 x 4 on two others.
 #ifndef BDL_SAMPLE_BPC
 #define BDL_SAMPLE_BPC 2
 #endif
 
-template <int NOISE, bool FL>
+template <int NOISE, bool FL, int U>
 SampleKernel pick_sample_n(int var_mode, bool m2, bool recip) {
-  constexpr int U = BDL_SAMPLE_U;
   if (!m2) return bdl_sample_kernel<BDL_VAR_GIVEN, false, false, NOISE, FL, U>;
   switch (var_mode) {
     case BDL_VAR_RAW_MOMENTS: return bdl_sample_kernel<BDL_VAR_RAW_MOMENTS, true, false, NOISE, FL, U>;
@@ -458,13 +456,20 @@ SampleKernel pick_sample_n(int var_mode, bool m2, bool recip) {
   }
 }
 
-// floored: var_floor >= 2^-96 (the Runners' 1e-12 clamp), see sqrt_floored
-SampleKernel pick_sample(int var_mode, bool m2, bool recip, int noise_mode, bool floored) {
+template <int U>
+SampleKernel pick_sample_u(int var_mode, bool m2, bool recip, int noise_mode, bool floored) {
   if (noise_mode == BDL_NOISE_BUFFER)
-    return floored ? pick_sample_n<BDL_NOISE_BUFFER, true>(var_mode, m2, recip)
-                   : pick_sample_n<BDL_NOISE_BUFFER, false>(var_mode, m2, recip);
-  return floored ? pick_sample_n<BDL_NOISE_PHILOX, true>(var_mode, m2, recip)
-                 : pick_sample_n<BDL_NOISE_PHILOX, false>(var_mode, m2, recip);
+    return floored ? pick_sample_n<BDL_NOISE_BUFFER, true, U>(var_mode, m2, recip)
+                   : pick_sample_n<BDL_NOISE_BUFFER, false, U>(var_mode, m2, recip);
+  return floored ? pick_sample_n<BDL_NOISE_PHILOX, true, U>(var_mode, m2, recip)
+                 : pick_sample_n<BDL_NOISE_PHILOX, false, U>(var_mode, m2, recip);
+}
+
+// floored: var_floor >= 2^-96 (the Runners' 1e-12 clamp), see sqrt_floored
+SampleKernel pick_sample(int var_mode, bool m2, bool recip, int noise_mode, bool floored,
+                         int unroll) {
+  return unroll == 1 ? pick_sample_u<1>(var_mode, m2, recip, noise_mode, floored)
+                     : pick_sample_u<4>(var_mode, m2, recip, noise_mode, floored);
 }
 
 __global__ __launch_bounds__(kBlock) void bdl_philox_kernel(float* __restrict__ out, int64_t n,
@@ -523,8 +528,8 @@ int grid_for(int64_t ngroups, int per_block_groups) {
   return (int)std::max<int64_t>(1, std::min(want, cap));
 }
 
-int grid_sample(int64_t ngroups, int blocks_per_cu) {
-  const int64_t per_block = (int64_t)kBlock * BDL_SAMPLE_U;
+int grid_sample(int64_t ngroups, int blocks_per_cu, int unroll) {
+  const int64_t per_block = (int64_t)kBlock * unroll;
   const int64_t want = (ngroups + per_block - 1) / per_block;
   const int64_t cap = (int64_t)device_cu_count() * (blocks_per_cu > 0 ? blocks_per_cu : BDL_SAMPLE_BPC);
   return (int)std::max<int64_t>(1, std::min(want, cap));
@@ -998,13 +1003,16 @@ int bdl_posterior_sample(const bdl_sample_args* s, void* stream) {
                 "index below 2^32");
   if (s->blocks_per_cu < 0 || s->blocks_per_cu > 8)
     return fail(BDL_ERR_ARG, "bdl_posterior_sample: blocks_per_cu in [0, 8]");
+  if (s->unroll != 0 && s->unroll != 1 && s->unroll != 4)
+    return fail(BDL_ERR_ARG, "bdl_posterior_sample: unroll 0 (default 4), 1 or 4");
+  const int su = s->unroll == 1 ? 1 : 4;
   SArgs a{s->out, s->mom1, s->mom2, s->noise, s->n, s->var_mode, s->noise_mode,
           s->ratio, s->var_floor, s->inv_ratio, s->seed, s->chain, s->step,
           (uint32_t)s->chain_groups};
   const bool floored = s->var_floor >= 0x1p-96f;  // false for NaN
   hipLaunchKernelGGL(pick_sample(s->var_mode, s->mom2 != nullptr, s->inv_ratio != 0.0f,
-                                 s->noise_mode, floored),
-                     dim3(grid_sample((s->n + 3) / 4, s->blocks_per_cu)), dim3(kBlock), 0,
+                                 s->noise_mode, floored, su),
+                     dim3(grid_sample((s->n + 3) / 4, s->blocks_per_cu, su)), dim3(kBlock), 0,
                      (hipStream_t)stream, a);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) {

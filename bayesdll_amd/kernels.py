@@ -253,28 +253,29 @@ def moments_update(theta, mom1, mom2, collect, collect_a=1.0, collect_b=1.0, div
             "bdl_moments_update")
 
 
-SAMPLE_BPC_CANDIDATES = (2, 3, 4)  # workgroups per CU tried for a vector's draw
-SAMPLE_TUNE_MIN = 1 << 24          # smaller draws keep the default (2)
-_SAMPLE_BPC = {}                   # (device index, n) -> workgroups per CU
+# (workgroups per CU, float4 groups per lane) tried for a vector's draw
+SAMPLE_GEOMETRIES = ((2, 4), (3, 4), (4, 4), (4, 1), (6, 1))
+SAMPLE_TUNE_MIN = 1 << 22          # smaller draws keep the default (2 x 4)
+_SAMPLE_GEOM = {}                  # (device index, n) -> (workgroups per CU, unroll)
 
 
 def sample_geometry(n, device):
-    """The posterior draw's tuned workgroups per CU for an n-element vector on
-    `device` (None until posterior_sample tuned it)."""
-    return _SAMPLE_BPC.get((torch.device(device).index, int(n)))
+    """The posterior draw's tuned (workgroups per CU, unroll) for an n-element
+    vector on `device` (None until posterior_sample tuned it)."""
+    return _SAMPLE_GEOM.get((torch.device(device).index, int(n)))
 
 
 def _tune_sample(a, out):
-    """Time the draw at each SAMPLE_BPC_CANDIDATES geometry with its own
-    arguments (each launch writes the same values: same keys), keep the
-    fastest.  Why: the bare access mix of the draw's buffers ranked 3
-    workgroups/CU x 4 ahead of the compiled-in 2 x 4 by 4 % on one box
-    (bench.py aux_kernels.posterior_sample.mix_ceiling), and round 2's probes
-    ranked 2 x 4 first on two others."""
+    """Time the draw at each SAMPLE_GEOMETRIES entry with its own arguments
+    (each launch writes the same values: same keys), keep the fastest.  Why:
+    the bare access mix of the draw's buffers ranked 3 workgroups/CU x 4
+    first at ViT-L/32 size and 4 x 1 at ResNet-101 size on one box (bench.py
+    aux_kernels.posterior_sample.mix_ceiling, profiles/round4/methods/), and
+    round 2's probes ranked 2 x 4 first on two others."""
     stream = L.current_stream_handle(out.device)
     best = None
-    for bpc in SAMPLE_BPC_CANDIDATES:
-        a.blocks_per_cu = bpc
+    for bpc, u in SAMPLE_GEOMETRIES:
+        a.blocks_per_cu, a.unroll = bpc, u
         L.check(L.lib().bdl_posterior_sample(a, stream), "bdl_posterior_sample")
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
@@ -284,17 +285,17 @@ def _tune_sample(a, out):
         ev[1].synchronize()
         ms = ev[0].elapsed_time(ev[1])
         if best is None or ms < best[0]:
-            best = (ms, bpc)
+            best = (ms, (bpc, u))
     return best[1]
 
 
 def posterior_sample(out, mom1, mom2, *, var_mode, ratio=1.0, var_floor=1e-12, noise=None,
-                     seed=0, chain=0, step=0, div_mode=None, chain_groups=0, blocks_per_cu=None):
+                     seed=0, chain=0, step=0, div_mode=None, chain_groups=0, geometry=None):
     """out = mom1 + sqrt(clamp(var(mom1, mom2), var_floor)) * eps (eps: buffer or Philox;
     chain_groups > 0: stacked chains keyed chain + k, bdl_sample_args.chain_groups).
-    blocks_per_cu: the launch's workgroups per CU; None = tuned once per device
-    and size on the first draw of >= SAMPLE_TUNE_MIN elements (outside graph
-    capture), 2 below.  Values never depend on it."""
+    geometry: (workgroups per CU, unroll 1 or 4) of the launch; None = tuned
+    once per device and size on the first draw of >= SAMPLE_TUNE_MIN elements
+    (outside graph capture), 2 x 4 below.  Values never depend on it."""
     L.require_hip(out, "out")
     a = L.SampleArgs()
     a.out, a.mom1 = out.data_ptr(), mom1.data_ptr()
@@ -309,13 +310,13 @@ def posterior_sample(out, mom1, mom2, *, var_mode, ratio=1.0, var_floor=1e-12, n
     a.inv_ratio = _inv(ratio) if _div_flag(div_mode) else 0.0
     a.seed, a.chain, a.step = int(seed), int(chain), int(step) & 0xFFFFFFFFFFFFFFFF
     a.chain_groups = int(chain_groups)
-    if blocks_per_cu is None:
+    if geometry is None:
         key = (out.device.index, int(a.n))
-        blocks_per_cu = _SAMPLE_BPC.get(key, 0)
-        if not blocks_per_cu and a.n >= SAMPLE_TUNE_MIN and \
+        geometry = _SAMPLE_GEOM.get(key)
+        if geometry is None and a.n >= SAMPLE_TUNE_MIN and \
                 not torch.cuda.is_current_stream_capturing():
-            blocks_per_cu = _SAMPLE_BPC[key] = _tune_sample(a, out)
-    a.blocks_per_cu = int(blocks_per_cu)
+            geometry = _SAMPLE_GEOM[key] = _tune_sample(a, out)
+    a.blocks_per_cu, a.unroll = (int(x) for x in (geometry or (0, 0)))
     L.check(L.lib().bdl_posterior_sample(a, L.current_stream_handle(out.device)),
             "bdl_posterior_sample")
 
@@ -367,8 +368,11 @@ AUTOTUNE_CANDIDATES = ((2, 1, 1), (1, 4, 1), (3, 1, 1), (2, 4, 1), (1, 2, 1), (2
 # Adam-SGHMC 1 x 1 by 1.5 % and 4 x 4 by 0.3 % over 2 x 4 (seven streams: fewer
 # accesses in flight per CU pay); cSGHMC 1 x 4 by >= 1.9 % over every other
 AUTOTUNE_BY_METHOD = {
-    "csghmc": AUTOTUNE_CANDIDATES,
-    "sgld": AUTOTUNE_CANDIDATES + ((3, 4, 1), (4, 4, 1)),
+    # + 1 x 1 and 3 x 4: the bare access mix of the SGLD buffers ran 1 x 1 8 %
+    # ahead of the tuned 2 x 1 at ResNet-101 size, and of the explore buffers
+    # 3 x 4 first at ViT-L/32 size (bench.py mix_ceiling, profiles/round4/methods/)
+    "csghmc": AUTOTUNE_CANDIDATES + ((3, 4, 1),),
+    "sgld": AUTOTUNE_CANDIDATES + ((3, 4, 1), (4, 4, 1), (1, 1, 1)),
     "adam": AUTOTUNE_CANDIDATES + ((1, 1, 1), (4, 4, 1)),
 }
 _TUNED = {}

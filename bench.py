@@ -319,10 +319,10 @@ def aux_kernels(st, reps=20):
         res["posterior_sample"]["out_kept"] = dinfo["kept"]
     res["posterior_sample"]["moments"] = "flat.moment_pair"
     # the draw's own launch geometry: its tuned workgroups/CU x 4 groups
-    bpc = K.sample_geometry(n, st.device) or 2
-    res["posterior_sample"]["blocks_per_cu"] = bpc
+    geo = K.sample_geometry(n, st.device) or (2, 4)
+    res["posterior_sample"]["geometry"] = f"{geo[0]}wg/cu x{geo[1]}"
     res["posterior_sample"]["mix_ceiling"] = mix_ceiling(
-        [m1, m2], [out], (bpc, 4), res["posterior_sample"]["avg_ms"])
+        [m1, m2], [out], geo, res["posterior_sample"]["avg_ms"])
     del m1, m2, out
     # the running moments of sgld / sghmc (methods/sgld.py:95-102 seeds them
     # from theta at burn-in), allocated as the sgld Runner allocates them:

@@ -286,6 +286,8 @@ typedef struct bdl_sample_args {
   int32_t blocks_per_cu;   /* workgroups per CU, 1-8 (0: 2); the caller may tune it (ABI v7) */
   uint64_t seed, chain, step;
   uint64_t chain_groups;   /* stacked chains, as bdl_step_args.chain_groups (0: one) */
+  int32_t unroll;          /* float4 groups per lane in flight: 0 (= 4), 1 or 4 (ABI v7) */
+  int32_t pad;
 } bdl_sample_args;
 
 int bdl_version(void);

@@ -962,9 +962,9 @@ def test_moment_pair_changes_nothing_but_the_addresses(monkeypatch):
 
 
 def test_posterior_draw_geometry_changes_nothing_and_is_tuned_once():
-    """bdl_sample_args.blocks_per_cu (ABI v7): every geometry draws the same
-    bits; kernels.posterior_sample tunes it once per device and size for
-    vectors of >= SAMPLE_TUNE_MIN elements and reuses the choice."""
+    """bdl_sample_args.blocks_per_cu / unroll (ABI v7): every geometry draws
+    the same bits; kernels.posterior_sample tunes it once per device and size
+    for vectors of >= SAMPLE_TUNE_MIN elements and reuses the choice."""
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
     n = K.SAMPLE_TUNE_MIN + 4093
@@ -972,22 +972,24 @@ def test_posterior_draw_geometry_changes_nothing_and_is_tuned_once():
     m1 = torch.randn(n, device=DEV, generator=g) * 0.02
     m2 = torch.rand(n, device=DEV, generator=g) * 1e-4
     outs = []
-    for bpc in (1, 2, 3, 4, 8):
+    for geo in ((1, 4), (2, 4), (3, 4), (4, 1), (8, 1), (0, 0)):
         out = torch.empty(n, device=DEV)
         K.posterior_sample(out, m1, m2, var_mode=L.VAR_WELFORD, ratio=3.0, seed=5, chain=2,
-                           step=7, blocks_per_cu=bpc)
+                           step=7, geometry=geo)
         outs.append(out)
     torch.cuda.synchronize()
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
-    K._SAMPLE_BPC.pop((torch.device(DEV).index or 0, n), None)
+    K._SAMPLE_GEOM.pop((torch.device(DEV).index or 0, n), None)
     out = torch.empty(n, device=DEV)
     K.posterior_sample(out, m1, m2, var_mode=L.VAR_WELFORD, ratio=3.0, seed=5, chain=2, step=7)
     torch.cuda.synchronize()
-    assert K.sample_geometry(n, out.device) in K.SAMPLE_BPC_CANDIDATES
+    assert K.sample_geometry(n, out.device) in K.SAMPLE_GEOMETRIES
     assert torch.equal(out, outs[0])
     with pytest.raises(RuntimeError, match="blocks_per_cu"):
-        K.posterior_sample(out, m1, m2, var_mode=L.VAR_WELFORD, ratio=3.0, blocks_per_cu=9)
+        K.posterior_sample(out, m1, m2, var_mode=L.VAR_WELFORD, ratio=3.0, geometry=(9, 4))
+    with pytest.raises(RuntimeError, match="unroll"):
+        K.posterior_sample(out, m1, m2, var_mode=L.VAR_WELFORD, ratio=3.0, geometry=(2, 2))
 
 
 @pytest.mark.parametrize("nr,nw", [(2, 1), (3, 2), (4, 2), (3, 4), (5, 4), (7, 5)])
