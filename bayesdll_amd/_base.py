@@ -149,16 +149,7 @@ class FusedModelBase(nn.Module):
             self.release_graphs()  # graphs captured against the old state's buffers
             if self.noise_mode not in NOISE_MODES:
                 raise ValueError(f"noise_mode must be one of {NOISE_MODES}")
-            # launch geometry for this device and size (speed only: results
-            # never depend on it), tuned BEFORE the chain's vectors exist: the
-            # tuning's scratch vectors are placed with the chain's roles, and
-            # their placed set, parked when they die, becomes the chain's
-            # (bayesdll_amd.placement pool: one placement search, not two)
             from . import kernels as K
-            params = list(net.parameters())
-            n_all = sum(p.numel() for p in params)
-            launch_cfg = K.autotune_once(n_all, params[0].device, self.tune_method) \
-                if params and params[0].is_cuda else None
             self._state = FlatState(net, net0, readout_name=getattr(net, "readout_name", None),
                                     bias=getattr(self, "bias", "informative"),
                                     need_prior=self.need_prior, need_mom=self.need_mom,
@@ -168,10 +159,13 @@ class FusedModelBase(nn.Module):
             steps_timed = int(os.environ.get("BDL_STEP_TIMING", "0") or 0)
             if steps_timed > 0:  # sampled update timing, logged once per epoch
                 self._state.timer = K.StepTimer(steps_timed)
-            self._state.launch_cfg = launch_cfg
-            if launch_cfg is not None:
-                self._state.collect_cfg = K.collect_config(n_all, params[0].device,
-                                                           self.tune_method)
+            # launch geometry (speed only: results never depend on it), tuned
+            # on the chain's OWN vectors at the first launch of each kind
+            # (plain step, collect step) with that launch's arguments, the
+            # vectors it writes restored after every candidate
+            # (kernels.request_state_tuning)
+            self._state.launch_cfg = self._state.collect_cfg = None
+            K.request_state_tuning(self._state, self.tune_method)
         return self._state
 
     @property

@@ -145,11 +145,17 @@ class StepTimer:
         return out
 
 
-def _launch(state, fn, a, adam=None):
+def _launch(state, fn, a, adam=None, written=None):
     # the steady-state collect kinds (m1 / m2 read and written) have their own
     # geometry; the cycle's first collect (m1 / m2 only written) runs at the
     # step's: 1.42 ms there vs 1.48 at the Welford collect's 1 x 1
-    _use_geometry(state, a.collect in (L.COLLECT_WELFORD, L.COLLECT_MEAN))
+    collect = a.collect in (L.COLLECT_WELFORD, L.COLLECT_MEAN)
+    pend = getattr(state, "_tune_pending", None)
+    if pend and written is not None and int(a.n) == int(state.n) and \
+            ("collect" if collect else "step") in pend and \
+            not torch.cuda.is_current_stream_capturing():
+        _tune_kind(state, fn, collect, written)
+    _use_geometry(state, collect)
     t = getattr(state, "timer", None)
     e0 = t.begin() if t is not None else None
     fn()
@@ -157,11 +163,30 @@ def _launch(state, fn, a, adam=None):
         t.end(e0, alg_bytes_per_elem(a, adam) * int(a.n))
 
 
+def _written(state, method, *, grad_only, mom, extra=(), mom1=None, mom2=None):
+    """The vectors a full step launch writes (saved and restored while it is
+    tuned on the state's own buffers), or None when they are not all flat
+    vectors of the state (per-tensor gradients written by a *_GRAD method)."""
+    if grad_only:
+        if getattr(state, "grad", None) is None:
+            return None
+        out = [state.grad]
+    else:
+        out = [state.theta]
+    out += [t for t in (mom,) + tuple(extra) + (mom1, mom2) if t is not None]
+    return out
+
+
 def sgmcmc_step(state, method, **kw):
     """One fused update over `state` (a FlatState). Asynchronous."""
     a = _step_args(state, method, **kw)
+    mb = kw.get("mom_buf")
+    wr = _written(state, method, grad_only=method in (L.SGHMC_GRAD, L.SGLD_GRAD),
+                  mom=state.mom if mb is None else mb,
+                  mom1=kw.get("mom1") if kw.get("collect", L.COLLECT_NONE) else None,
+                  mom2=kw.get("mom2") if kw.get("collect", L.COLLECT_NONE) else None)
     _launch(state, lambda: L.check(L.lib().bdl_sgmcmc_step(a, L.current_stream_handle(state.device)),
-                                   "bdl_sgmcmc_step"), a)
+                                   "bdl_sgmcmc_step"), a, written=wr)
 
 
 def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps, t,
@@ -197,8 +222,12 @@ def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps,
     ad.grad_is_mom = 1 if grad_is_mom else 0
     if tile is not None:
         ad.tile_log2, ad.tile_streams, ad.tile_mask = (int(x) for x in tile)
+    wr = _written(state, method, grad_only=method == L.ADAM_SGHMC_GRAD, mom=state.mom,
+                  extra=(adam_m, adam_v) + ((sgd_buf,) if sgd_buf is not None else ()),
+                  mom1=mom1 if collect != L.COLLECT_NONE else None,
+                  mom2=mom2 if collect != L.COLLECT_NONE else None)
     _launch(state, lambda: L.check(L.lib().bdl_adam_step(a, ad, L.current_stream_handle(state.device)),
-                                   "bdl_adam_step"), a, ad)
+                                   "bdl_adam_step"), a, ad, written=wr)
 
 
 def stream_mix(reads, writes, blocks_per_cu=1, unroll=4):
@@ -522,6 +551,87 @@ def autotune(n, device=None, reps=6, candidates=None, method="csghmc", placed=Tr
     gc.collect()  # the scratch state now, so that its placed set is parked for the chain
     torch.cuda.empty_cache()
     return res
+
+
+TUNE_ON_STATE_MIN = 1 << 16  # smaller states keep the default geometry
+
+
+def request_state_tuning(state, method):
+    """Tune `state`'s launch geometry on its OWN buffers at the first full
+    launch of each kind (the plain step; the collect step), with that launch's
+    own arguments, restoring every vector it writes after each candidate (so
+    the chain is unchanged; the update never depends on geometry anyway).
+    Why not scratch vectors (autotune): which geometry is fastest depends on
+    where the vectors sit in HBM — on one box the SGLD sweep over ResNet-101
+    ran 2 x 4 fastest on scratch vectors while the bare access mix of the
+    chain's own buffers ran 1 x 1 8 % ahead of it, and the Adam sweep's best
+    moved from 2 x 4 to 1 x 4 (bench.py mix_ceiling, profiles/round4/methods_b/).
+    BDL_AUTOTUNE=0: the defaults."""
+    if os.environ.get("BDL_AUTOTUNE", "1") == "0" or int(state.n) < TUNE_ON_STATE_MIN:
+        return
+    state._tune_pending = {"step", "collect"}
+    state._tune_method = method
+    state.tuned = {}
+
+
+def _tune_kind(state, fn, collect, written):
+    kind = "collect" if collect else "step"
+    state._tune_pending.discard(kind)
+    cands = tuple(AUTOTUNE_BY_METHOD.get(state._tune_method, AUTOTUNE_CANDIDATES))
+    if collect:
+        cands += tuple(c for c in COLLECT_EXTRA if c not in cands)
+    nf = getattr(state, "nonfinite", None)
+    best, times = tune_on_state(fn, list(written) + ([nf] if nf is not None else []), cands,
+                                state.device)
+    if collect:
+        state.collect_cfg = best
+    else:
+        state.launch_cfg = best
+    state.tuned[kind] = {"best": best, "ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4)
+                                              for c, t in times.items()}}
+
+
+def tune_on_state(launch, written, candidates, device, reps=4):
+    """Time `launch` (a zero-argument launch over a state's own buffers) at
+    each candidate geometry — round 1 every candidate, round 2 the three
+    fastest again with twice the repetitions, averaged — restoring the
+    `written` tensors after every candidate.  Returns (best, {cfg: ms}); the
+    previous geometry is re-installed."""
+    import numpy as np
+    saved = [w.clone() for w in written]
+    prev = _ACTIVE[0]
+
+    def measure(cfgs, k):
+        out = {}
+        for cfg in cfgs:
+            set_launch_config(*cfg)
+            launch()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(k)]
+            for e0, e1 in ev:
+                e0.record()
+                launch()
+                e1.record()
+            torch.cuda.synchronize(device)
+            out[cfg] = float(np.median([x.elapsed_time(y) for x, y in ev]))
+            for w, s in zip(written, saved):
+                w.copy_(s)
+        return out
+
+    try:
+        times = measure(candidates, reps)
+        top = sorted(times, key=times.get)[:3]
+        again = measure(top, 2 * reps)
+        for cfg in top:
+            times[cfg] = 0.5 * (times[cfg] + again[cfg])
+        best = min(top, key=times.get)
+    finally:
+        for w, s in zip(written, saved):
+            w.copy_(s)
+        del saved
+        if prev is not None:
+            set_launch_config(*prev)
+    return best, times
 
 
 def prewarm(n, device=None, method="csghmc", seconds=2.5):

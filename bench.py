@@ -532,26 +532,18 @@ def main():
     prewarm = {"seconds": a.prewarm_seconds,
                "launches": K.prewarm(n_all, local, tune_method, a.prewarm_seconds)
                if a.prewarm_seconds > 0 else 0}
-    tuned = None
+    tune_on_state = False
     if a.blocks_per_cu or a.unroll or a.grid_stride >= 0:
         K.set_launch_config(a.blocks_per_cu, a.unroll, max(a.grid_stride, 0))
         launch = {"blocks_per_cu": a.blocks_per_cu, "unroll": a.unroll,
                   "grid_stride": max(a.grid_stride, 0), "autotuned": False}
     elif not a.no_autotune:
-        # untimed setup (like cudnn.benchmark): pick the launch geometry for
-        # this device; results are identical under every geometry
-        # (its scratch vectors placed like the chain's: their parked set becomes
-        # the chain's, bayesdll_amd.placement)
-        best, tuned, cbest, ctuned = K.autotune(n_all, device=local, method=tune_method,
-                                                placed=placed, collect=True)
-        launch = {"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
-                  "autotuned": True,
-                  "candidates_ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4) for c, t in tuned.items()},
-                  "tuned_on": a.method,
-                  # the collect steps' own geometry (kernels._use_geometry)
-                  "collect": {"blocks_per_cu": cbest[0], "unroll": cbest[1],
-                              "candidates_ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4)
-                                                for c, t in ctuned.items()}}}
+        # untimed setup (like cudnn.benchmark): the launch geometry is tuned on
+        # the chain's OWN vectors, as the Runners tune it, once the state
+        # exists (below); results are identical under every geometry
+        tune_on_state = True
+        launch = {"autotuned": True, "tuned_on": f"{a.method} on the chain's own vectors "
+                                                 "(kernels.request_state_tuning)"}
     else:
         launch = {"default": True, "autotuned": False}
     dev = torch.device("cuda", local)
@@ -560,8 +552,6 @@ def main():
     st = FlatState.from_segments(segs, readout, device=dev, need_prior=sgld,
                                  placement=tune_method if placed else None,
                                  extra=("adam_m", "adam_v", "sgd_buf") if adam else ())
-    if launch.get("autotuned"):
-        st.launch_cfg, st.collect_cfg = best, cbest
     gen = torch.Generator(device=dev).manual_seed(42 + rank)
     if sgld:  # config 3: theta0 ~ N(0, 0.02^2) (pretrained stand-in), theta = theta0 + N(0, 1e-3^2)
         st.prior.normal_(0.0, 0.02, generator=gen)
@@ -692,6 +682,54 @@ def main():
 
     if sgld:
         step = adam_step if adam else sgld_step  # noqa: F811
+    if tune_on_state:
+        # the first launch of each kind (plain step, collect step) tunes the
+        # geometry on this state's buffers with its own arguments (every vector
+        # it writes restored after each candidate), then runs once; the state
+        # is restored from a snapshot afterwards, so the run starts where it was
+        K.request_state_tuning(st, tune_method)
+        cyc = min(m1s) if m1s else None
+        touched = [st.theta, st.mom] + ([st.extra[k] for k in ("adam_m", "adam_v", "sgd_buf")]
+                                        if adam else []) + \
+            ([m1s[cyc], m2s[cyc]] if cyc is not None else [])
+        snap = [v.clone() for v in touched]
+        kw = dict(seed=42 + rank, chain=rank, step=0)
+        for collect in (False, True):
+            if adam:
+                K.adam_step(st, L.ADAM_SGHMC, adam_m=adam_m, adam_v=adam_v, sgd_buf=sgd_buf,
+                            beta1=0.9, beta2=0.999, eps=1e-8, t=2, momentum_decay=alpha, nd=nd,
+                            lrs=(lr, lr_head), noise_mode=L.NOISE_PHILOX,
+                            sigma2=prior_sig ** 2, n_data=N, mu=mu, momentum=True,
+                            collect=L.COLLECT_MEAN if collect else L.COLLECT_NONE,
+                            mom1=m1s[cyc], mom2=m2s[cyc], collect_a=1.0, collect_b=2.0, **kw)
+            elif sgld:
+                K.sgmcmc_step(st, L.SGLD, lrs=(lr, lr_head),
+                              noise_scale=[nd * np.sqrt(2 / (N * x)) for x in (lr, lr_head)],
+                              noise_mode=L.NOISE_PHILOX, prior_sig=prior_sig,
+                              sigma2=prior_sig ** 2, n_data=N, mu=mu, momentum=True,
+                              collect=L.COLLECT_MEAN if collect else L.COLLECT_NONE,
+                              mom1=m1s[cyc], mom2=m2s[cyc], collect_a=1.0, collect_b=2.0, **kw)
+            else:
+                K.sgmcmc_step(st, L.CSGHMC, lrs=(lr, lr_head),
+                              noise_scale=(1e-7, 1e-7) if collect else (0.0, 0.0),
+                              noise_mode=L.NOISE_PHILOX if collect else L.NOISE_NONE,
+                              one_minus_alpha=1 - alpha, prior_sig=prior_sig,
+                              collect=L.COLLECT_WELFORD if collect else L.COLLECT_NONE,
+                              mom1=m1s[cyc] if collect else None,
+                              mom2=m2s[cyc] if collect else None, collect_a=3.0, **kw)
+        torch.cuda.synchronize()
+        for v, s0 in zip(touched, snap):
+            v.copy_(s0)
+        del snap
+        best, cbest = st.launch_cfg, st.collect_cfg
+        if best is None or cbest is None:  # BDL_AUTOTUNE=0: the defaults
+            best = cbest = (2, 1, 1)
+            st.tuned = {"step": {"ms": None}, "collect": {"ms": None}}
+        launch.update({"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
+                       "candidates_ms": st.tuned["step"]["ms"],
+                       # the collect steps' own geometry (kernels._use_geometry)
+                       "collect": {"blocks_per_cu": cbest[0], "unroll": cbest[1],
+                                   "candidates_ms": st.tuned["collect"]["ms"]}})
     for k in range(a.warmup):
         step(k)
     torch.cuda.synchronize()

@@ -132,3 +132,46 @@ def test_adam_tiled_state_equals_separate_vectors(tile_log2):
     ref = outs[("separate", (1, 4, 1))]
     for k, o in outs.items():
         assert torch.equal(o, ref), k
+
+
+@pytest.mark.parametrize("method", ["csghmc", "sgld"])
+def test_tuning_on_the_state_leaves_the_chain_unchanged(method):
+    """kernels.request_state_tuning (the Runners' and bench.py's geometry
+    tuning): the first launch of each kind times every candidate on the
+    state's own vectors with that launch's arguments and restores what they
+    wrote, so the chain equals one run at a fixed geometry bit for bit; the
+    tuned geometries are installed per kind."""
+    from bayesdll_amd import kernels as K
+    n = (1 << 20) + 13
+    outs = []
+    try:
+        for tune in (False, True):
+            st, L = _state(n, 9)
+            m1 = torch.zeros(n, device="cuda")
+            m2 = torch.zeros(n, device="cuda")
+            K.set_launch_config(2, 1, 1)
+            if tune:
+                K.request_state_tuning(st, method)
+            for t in range(3):
+                collect = L.COLLECT_WELFORD if method == "csghmc" else L.COLLECT_MEAN
+                ck = dict(collect=collect, mom1=m1, mom2=m2, collect_a=float(t + 1),
+                          collect_b=float(t + 2)) if t == 2 else {}
+                if method == "csghmc":
+                    K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-3, 2e-3), noise_scale=(1e-2, 2e-2),
+                                  noise_mode=L.NOISE_PHILOX, one_minus_alpha=0.9, prior_sig=1.0,
+                                  seed=3, chain=1, step=t, **ck)
+                else:
+                    K.sgmcmc_step(st, L.SGLD, lrs=(1e-3, 2e-3), noise_scale=(1e-2, 2e-2),
+                                  noise_mode=L.NOISE_PHILOX, prior_sig=1.0, sigma2=1.0,
+                                  n_data=100.0, mu=0.5, first_step=t == 0, momentum=True,
+                                  seed=3, chain=1, step=t, **ck)
+            torch.cuda.synchronize()
+            outs.append(torch.cat([st.theta, st.mom, m1, m2]).clone())
+            if tune:
+                assert set(st.tuned) == {"step", "collect"} and not st._tune_pending
+                assert st.launch_cfg in K.AUTOTUNE_BY_METHOD[method]
+                assert st.collect_cfg is not None
+                assert int(st.nonfinite.item()) == 0
+    finally:
+        K.set_launch_config(0, 0, 0)
+    assert torch.equal(outs[0], outs[1])
