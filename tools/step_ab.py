@@ -33,12 +33,14 @@ def use(path):
     L.lib()
 
 
-METHOD = os.environ.get("METHOD", "csghmc")  # or "adam": the Adam-SGHMC + SGD step
+METHOD = os.environ.get("METHOD", "csghmc")  # or "adam" (Adam-SGHMC + SGD), "sgld" (+ SGD)
 use(libs[0])
-segs, readout = segments("vit_l_32", 1000)
+segs, readout = segments(os.environ.get("BACKBONE", "vit_l_32"), 1000)
 adam = METHOD == "adam"
-st = FlatState.from_segments(segs, readout, device=dev, placement="adam" if adam else "csghmc",
-                             need_prior=adam,
+sgld = METHOD == "sgld"
+st = FlatState.from_segments(segs, readout, device=dev,
+                             placement=None if os.environ.get("BDL_PLACEMENT", "0") == "0"
+                             else METHOD, need_prior=adam or sgld,
                              extra=("adam_m", "adam_v", "sgd_buf") if adam else ())
 gen = torch.Generator(device=dev).manual_seed(1)
 st.theta.normal_(0.0, 0.02, generator=gen)
@@ -53,6 +55,11 @@ lrs, alpha, N = (1e-4, 1e-2), 0.18, 1840.0
 
 
 def explore(i):
+    if sgld:  # methods/sgld.py:469-484 + SGD(momentum 0.5), Philox
+        K.sgmcmc_step(st, L.SGLD, lrs=lrs, noise_scale=(1e-3, 1e-3), noise_mode=L.NOISE_PHILOX,
+                      prior_sig=1.0, sigma2=1.0, n_data=N * 1e3, mu=0.5, momentum=True,
+                      seed=3, chain=0, step=i)
+        return
     if adam:  # methods/adam_sghmc.py:458-553 + SGD(momentum 0.5), Philox
         K.adam_step(st, L.ADAM_SGHMC, adam_m=st.extra["adam_m"], adam_v=st.extra["adam_v"],
                     sgd_buf=st.extra["sgd_buf"], beta1=0.9, beta2=0.999, eps=1e-8, t=i + 2,
@@ -64,6 +71,12 @@ def explore(i):
 
 
 def collect(i):
+    if sgld:
+        K.sgmcmc_step(st, L.SGLD, lrs=lrs, noise_scale=(1e-3, 1e-3), noise_mode=L.NOISE_PHILOX,
+                      prior_sig=1.0, sigma2=1.0, n_data=N * 1e3, mu=0.5, momentum=True,
+                      collect=L.COLLECT_MEAN, mom1=m1, mom2=m2, collect_a=float(i + 1),
+                      collect_b=float(i + 2), seed=3, chain=0, step=i)
+        return
     ns = [0.01 * np.sqrt(2 * alpha * x) / N for x in lrs]
     K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_PHILOX,
                   one_minus_alpha=1 - alpha, prior_sig=1.0, collect=L.COLLECT_WELFORD, mom1=m1,
@@ -88,8 +101,9 @@ for r in range(rounds):
         use(path)
         for g in geoms:
             K.set_launch_config(*g)
-            for name, fn, bpe in (("adam" if adam else "explore", explore, 48 if adam else 20),
-                                  ("collect", collect, 36)):
+            for name, fn, bpe in (("adam" if adam else "sgld" if sgld else "explore", explore,
+                                   48 if adam else 24 if sgld else 20),
+                                  ("collect", collect, 40 if sgld else 36)):
                 if name == "collect" and (g != geoms[0] or adam):
                     continue
                 ms = t(fn)
