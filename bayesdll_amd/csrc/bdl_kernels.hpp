@@ -584,187 +584,6 @@ __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, i
 }
 
 
-// ---------------------------------------------------------------------------
-// Software-pipelined step sweep (A/B flavour -DBDL_STEP_PIPE; noise-bearing
-// kinds only: the explore sweep, with no noise, sits at its bare-mix ceiling
-// unpipelined): the next block iteration's loads are issued before this
-// iteration's Philox + update arithmetic, two register sets taking turns as in
-// adam_pipe_sweep; an iteration that needs the guarded path drains it.  Same
-// per-element update as chunk_fast / chunk_slow: bit-identical.
-// ---------------------------------------------------------------------------
-template <int U>
-struct StepRegs {
-  f4v th[U], g[U], v[U], t0[U], ep[U], m1[U], m2[U];
-};
-
-template <int METHOD, int NOISE, int COLLECT, int U>
-__device__ __forceinline__ void step_pipe_load(const KArgs& a, const StepConst& c, int64_t gb,
-                                               const float* gp, bool prior, bool gr,
-                                               StepRegs<U>& R) {
-  using T = StepTraits<METHOD, COLLECT>;
-  const f4v z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
-    R.v[u] = R.t0[u] = R.ep[u] = R.m1[u] = R.m2[u] = z;
-    R.th[u] = vload(a.theta + e);
-    R.g[u] = vload(gp + e);
-    if constexpr (T::kMom) R.v[u] = vload(a.mom + e);
-    if constexpr (METHOD == BDL_SGLD) {
-      if (c.sgd_mom_read) R.v[u] = vload(a.mom + e);
-    }
-    if constexpr (T::kReadPrior) {
-      if (prior && !gr) R.t0[u] = vload(a.prior_mean + e);
-    }
-    if constexpr (NOISE == BDL_NOISE_BUFFER) {
-      if (!gr) R.ep[u] = vload(a.noise + e);
-    }
-    if constexpr (T::kReadMoments) {
-      R.m1[u] = vload(a.mom1 + e);
-      if (c.has_m2) R.m2[u] = vload(a.mom2 + e);
-    }
-  }
-}
-
-template <int METHOD, int NOISE, int COLLECT, bool RECIP, int U, bool PRIOR, bool GR>
-__device__ __forceinline__ void step_pipe_compute(const KArgs& a, const StepConst& c, int64_t gb,
-                                                  float eta, float ns, float* gp, StepRegs<U>& R,
-                                                  uint32_t& bad) {
-  using T = StepTraits<METHOD, COLLECT>;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
-    const int64_t e = gi * 4;
-    if constexpr (NOISE == BDL_NOISE_PHILOX && !GR) R.ep[u] = step_noise4(a, gi);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float xt = R.th[u][j], xg = R.g[u][j], xv = R.v[u][j], x1 = R.m1[u][j], x2 = R.m2[u][j];
-      update_core<METHOD, NOISE, RECIP, PRIOR, GR>(a, c, eta, ns, xt, xg, xv, R.t0[u][j],
-                                                   R.ep[u][j]);
-      collect_core<COLLECT, RECIP>(a, c, xt, x1, x2);
-      R.th[u][j] = xt;
-      R.g[u][j] = xg;
-      R.v[u][j] = xv;
-      R.m1[u][j] = x1;
-      R.m2[u][j] = x2;
-    }
-    if constexpr (T::kWriteTheta) {
-      bad |= nonfinite4(R.th[u]);
-      vstore(a.theta + e, R.th[u]);
-    }
-    if constexpr (T::kWriteGrad) {
-      bad |= nonfinite4(R.g[u]);
-      vstore(gp + e, R.g[u]);
-    }
-    if constexpr (T::kMom) vstore(a.mom + e, R.v[u]);
-    if constexpr (METHOD == BDL_SGLD) {
-      if (c.sgd_mom) vstore(a.mom + e, R.v[u]);
-    }
-    if constexpr (T::kCollect) {
-      vstore(a.mom1 + e, R.m1[u]);
-      if (c.has_m2) vstore(a.mom2 + e, R.m2[u]);
-    }
-  }
-}
-
-struct StepPipeCursor {
-  int64_t gb;
-  int r;
-  uint32_t attr;
-  bool fast, loaded;
-};
-
-template <int U>
-__device__ __forceinline__ bool step_pipe_fast(const KArgs& a, int64_t gb, int& r,
-                                               uint32_t& attr) {
-  constexpr int64_t kIter = (int64_t)kBlock * U;
-  const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
-  if (gb >= ngroups) return false;
-  while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
-  const int64_t gend = min(gb + kIter, ngroups);
-  attr = run_attr(r);
-  return gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 && !(attr & kNoFastPath);
-}
-
-template <int METHOD, int NOISE, int COLLECT, bool RECIP, int U>
-__device__ __forceinline__ void step_pipe_dispatch(const KArgs& a, const StepConst& c,
-                                                   int64_t gb, uint32_t attr, float* gp,
-                                                   StepRegs<U>& R, uint32_t& bad) {
-  const bool head = (attr & BDL_ATTR_HEAD) != 0;
-  const float eta = head ? a.lr1 : a.lr0;
-  const float ns = head ? a.ns1 : a.ns0;
-  if constexpr (METHOD == BDL_CSGHMC) {
-    step_pipe_compute<METHOD, NOISE, COLLECT, RECIP, U, false, false>(a, c, gb, eta, ns, gp, R,
-                                                                      bad);
-  } else {
-    if constexpr (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) {
-      if (c.grad_ready) {
-        step_pipe_compute<METHOD, NOISE, COLLECT, RECIP, U, false, true>(a, c, gb, eta, ns, gp,
-                                                                         R, bad);
-        return;
-      }
-    }
-    if (attr & BDL_ATTR_PRIOR)
-      step_pipe_compute<METHOD, NOISE, COLLECT, RECIP, U, true, false>(a, c, gb, eta, ns, gp, R,
-                                                                       bad);
-    else
-      step_pipe_compute<METHOD, NOISE, COLLECT, RECIP, U, false, false>(a, c, gb, eta, ns, gp, R,
-                                                                        bad);
-  }
-}
-
-template <int METHOD, int NOISE, int COLLECT, bool RECIP, int U>
-__device__ __forceinline__ bool step_pipe_iter(const KArgs& a, const StepConst& c,
-                                               StepPipeCursor& k, StepRegs<U>& X,
-                                               StepRegs<U>& Y, uint32_t& bad) {
-  constexpr int64_t kIter = (int64_t)kBlock * U;
-  const int64_t ngroups = (a.n + 3) >> 2;
-  const int64_t gstep = (int64_t)gridDim.x * kIter;
-  if (k.gb >= ngroups) return false;
-  if (!k.fast) {
-    chunk_slow<METHOD, NOISE, COLLECT, RECIP, U>(a, c, k.gb, min(k.gb + kIter, ngroups), k.r, bad);
-    k.gb += gstep;
-    k.fast = step_pipe_fast<U>(a, k.gb, k.r, k.attr);
-    k.loaded = false;
-    return true;
-  }
-  float* gp = run_grad(a, k.r);
-  if (!k.loaded)
-    step_pipe_load<METHOD, NOISE, COLLECT, U>(a, c, k.gb, gp, (k.attr & BDL_ATTR_PRIOR) != 0,
-                                              c.grad_ready, X);
-  const int64_t nx = k.gb + gstep;
-  int rn = k.r;
-  uint32_t attrn = 0;
-  const bool fastn = step_pipe_fast<U>(a, nx, rn, attrn);
-  if (fastn)
-    step_pipe_load<METHOD, NOISE, COLLECT, U>(a, c, nx, run_grad(a, rn),
-                                              (attrn & BDL_ATTR_PRIOR) != 0, c.grad_ready, Y);
-  step_pipe_dispatch<METHOD, NOISE, COLLECT, RECIP, U>(a, c, k.gb, k.attr, gp, X, bad);
-  k.gb = nx;
-  k.r = rn;
-  k.attr = attrn;
-  k.fast = fastn;
-  k.loaded = fastn;
-  return true;
-}
-
-template <int METHOD, int NOISE, int COLLECT, bool RECIP, int U>
-__device__ __forceinline__ void step_pipe_sweep(const KArgs& a, const StepConst& c,
-                                                uint32_t& bad) {
-  constexpr int64_t kIter = (int64_t)kBlock * U;
-  StepPipeCursor k;
-  k.gb = (int64_t)blockIdx.x * kIter;
-  k.r = find_run_lds(a.nruns, k.gb * 4);
-  k.attr = 0;
-  k.fast = step_pipe_fast<U>(a, k.gb, k.r, k.attr);
-  k.loaded = false;
-  StepRegs<U> A, B;
-  for (;;) {
-    if (!step_pipe_iter<METHOD, NOISE, COLLECT, RECIP, U>(a, c, k, A, B, bad)) break;
-    if (!step_pipe_iter<METHOD, NOISE, COLLECT, RECIP, U>(a, c, k, B, A, bad)) break;
-  }
-}
-
 template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
 __device__ __forceinline__ void step_body(const KArgs& a) {
   StepConst c;
@@ -799,16 +618,6 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
 
   // stage the run table (and gradient bases) in LDS
   stage_runs(a);
-#ifdef BDL_STEP_PIPE
-  if constexpr (NOISE == BDL_NOISE_PHILOX) {
-    if (a.groups_per_block == 0) {  // grid-stride sweeps only
-      uint32_t badp = 0;
-      step_pipe_sweep<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, badp);
-      report_nonfinite(a, badp);
-      return;
-    }
-  }
-#endif
   if (g0 >= g1) return;
 
   int r = find_run_lds(a.nruns, g0 * 4);

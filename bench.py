@@ -444,6 +444,41 @@ def explore_tensor_grad_timing(st, reps=20):
     return res
 
 
+def explore_placed_timing(st, segs, readout, reps=20):
+    """Informational, after the timed region (--placement 0 runs only): the
+    explore step on a second chain state built with the opt-in physical-chunk
+    placement search (BDL_PLACEMENT=search, bayesdll_amd.placement), same
+    values and geometry as the timed state — what the opt-in buys on this box,
+    next to the default's number."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    from bayesdll_amd.flat import FlatState
+    prev = os.environ.get("BDL_PLACEMENT", "0")
+    os.environ["BDL_PLACEMENT"] = "search"
+    try:
+        ps = FlatState.from_segments(segs, readout, device=st.device, placement="csghmc")
+        ps.theta.copy_(st.theta)
+        ps.grad.copy_(st.grad)
+        ps.mom.copy_(st.mom)
+        ps.launch_cfg = getattr(st, "launch_cfg", None)
+
+        def fn(i):
+            K.sgmcmc_step(ps, L.CSGHMC, lrs=(1e-5, 1e-3), noise_scale=(0.0, 0.0),
+                          noise_mode=L.NOISE_NONE, one_minus_alpha=1 - 0.18, prior_sig=1.0,
+                          seed=0, chain=0, step=4_000_000 + i)
+        res = kind_stats(event_times(fn, reps, warm=2), BYTES_PER_ELEM["explore"], st.n)
+        info = ps.placement_info or {}
+        res["placement"] = {k: info.get(k) for k in ("allocator", "kept", "seconds", "chosen_ms",
+                                                      "untuned_torch_ms", "default_ms",
+                                                      "chunks_allocated", "transient_gb")}
+        del ps
+    finally:
+        os.environ["BDL_PLACEMENT"] = prev
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    return res
+
+
 def cpu_baseline(segs, readout, seconds):
     """The reference csghmc per-tensor update (oracle restatement, torch CPU,
     torch.randn_like per tensor) on the full ViT-L/32 shapes, timed for a
@@ -850,6 +885,12 @@ def main():
         ex["vs_flat_explore"] = round(ex["avg_ms"] / table["explore"]["avg_ms"], 4) \
             if "explore" in table else None
         table["explore_tensor_grad"] = dict(ex, launches=0, timed_region=False)
+    if not sgld and a.grad_mode == "flat" and a.placement == "0" and world == 1 and \
+            os.environ.get("BDL_BENCH_PLACED", "1") != "0":
+        ep = explore_placed_timing(st, segs, readout)
+        ep["vs_default_explore"] = round(ep["avg_ms"] / table["explore"]["avg_ms"], 4) \
+            if "explore" in table else None
+        table["explore_placed"] = dict(ep, launches=0, timed_region=False)
     out["methodology"] = {
         "timed_kinds": sorted(set(kinds)),
         "event_stride": timer.stride,
