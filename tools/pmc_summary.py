@@ -70,9 +70,13 @@ def main(tag, dest=None, backbone="vit_l_32"):
                         "bdl_adam_kernel" in nm}
         if step_kernels:
             nm = max(step_kernels, key=lambda k: len(step_kernels[k]))
-            durs = [d for _, d in step_kernels[nm]][-timed:]
+            # SKIP_LAST: launches of the same kernel after the timed region
+            # (bench.py explore_tensor_grad / explore_placed: 22 each)
+            skip = int(os.environ.get("SKIP_LAST", "0"))
+            durs = [d for _, d in step_kernels[nm]]
+            durs = (durs[:-skip] if skip else durs)[-timed:]
             json.dump({"kernel": nm, "timed_launches": len(durs),
-                       "avg_ns": round(sum(durs) / len(durs), 1),
+                       "avg_ns": round(sum(durs) / len(durs), 1), "skipped_last": skip,
                        "note": "mean of the last dispatches of the kernel the timed loop ran "
                                "(rocprofv3 --kernel-trace), to compare with bench.py's HIP-event "
                                "average for the same kernel"},
