@@ -554,6 +554,7 @@ def autotune(n, device=None, reps=6, candidates=None, method="csghmc", placed=Tr
 
 
 TUNE_ON_STATE_MIN = 1 << 16  # smaller states keep the default geometry
+TUNE_SNAPSHOT_FRACTION = 0.25  # the tuning's snapshot of the written vectors, at most this share of free HBM
 
 
 def request_state_tuning(state, method):
@@ -581,8 +582,16 @@ def _tune_kind(state, fn, collect, written):
     if collect:
         cands += tuple(c for c in COLLECT_EXTRA if c not in cands)
     nf = getattr(state, "nonfinite", None)
-    best, times = tune_on_state(fn, list(written) + ([nf] if nf is not None else []), cands,
-                                state.device)
+    written = list(written) + ([nf] if nf is not None else [])
+    # the snapshot of what the launch writes must fit comfortably: otherwise
+    # keep the current geometry (a model this large is tuned on nothing)
+    need = sum(w.numel() * w.element_size() for w in written)
+    free, _ = torch.cuda.mem_get_info(state.device)
+    if need > TUNE_SNAPSHOT_FRACTION * free:
+        state.tuned[kind] = {"skipped": f"snapshot {need >> 20} MiB > "
+                                        f"{TUNE_SNAPSHOT_FRACTION:g} x free {free >> 20} MiB"}
+        return
+    best, times = tune_on_state(fn, written, cands, state.device)
     if collect:
         state.collect_cfg = best
     else:

@@ -757,9 +757,10 @@ def main():
             v.copy_(s0)
         del snap
         best, cbest = st.launch_cfg, st.collect_cfg
-        if best is None or cbest is None:  # BDL_AUTOTUNE=0: the defaults
-            best = cbest = (2, 1, 1)
-            st.tuned = {"step": {"ms": None}, "collect": {"ms": None}}
+        if best is None or cbest is None:  # BDL_AUTOTUNE=0 / tuning skipped: the defaults
+            best = cbest = best or cbest or (2, 1, 1)
+            st.tuned = {k: dict(getattr(st, "tuned", {}).get(k, {}), ms=None)
+                        for k in ("step", "collect")}
         launch.update({"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
                        "candidates_ms": st.tuned["step"]["ms"],
                        # the collect steps' own geometry (kernels._use_geometry)
