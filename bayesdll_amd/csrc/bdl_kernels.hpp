@@ -21,13 +21,31 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes
 // counter = (group index lo32, chain lo32, step lo32, step hi32), key = seed.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+  // The key schedule is wave-uniform: left to itself the compiler hoists all
+  // twenty round keys (and the uniform counter words' xors) out of the sweep
+  // loop into SGPRs, which then spill into VGPR lanes (v_writelane /
+  // v_readlane + hazard s_nops in the hot loop).  BDL_PHILOX_KEYS_PER_CALL: an
+  // empty asm that "modifies" the keys keeps them per call (one s_add per
+  // round key).  Which schedule is faster depends on the kernel and its
+  // occupancy (1-4 % either way, same-process A/Bs: DESIGN.md §4), so the
+  // choice is made per translation unit in the Makefile, as is the xor form.
+#ifdef BDL_PHILOX_KEYS_PER_CALL
+  asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#ifdef BDL_PHILOX_TWO_XORS
     c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+#else
+    // gfx950's three-input bit op (truth table 0x96 = a ^ b ^ c): one VALU op
+    // per output word instead of two xors.
+    c = make_uint4(__builtin_amdgcn_bitop3_b32(hi1, c.y, k0, 0x96), lo1,
+                   __builtin_amdgcn_bitop3_b32(hi0, c.w, k1, 0x96), lo0);
+#endif
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }

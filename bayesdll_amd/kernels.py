@@ -283,7 +283,7 @@ def moments_update(theta, mom1, mom2, collect, collect_a=1.0, collect_b=1.0, div
 
 
 # (workgroups per CU, float4 groups per lane) tried for a vector's draw
-SAMPLE_GEOMETRIES = ((2, 4), (3, 4), (4, 4), (4, 1), (6, 1))
+SAMPLE_GEOMETRIES = ((1, 4), (2, 4), (3, 4), (4, 4), (4, 1), (6, 1))
 SAMPLE_TUNE_MIN = 1 << 22          # smaller draws keep the default (2 x 4)
 _SAMPLE_GEOM = {}                  # (device index, n) -> (workgroups per CU, unroll)
 
@@ -300,7 +300,10 @@ def _tune_sample(a, out):
     the bare access mix of the draw's buffers ranked 3 workgroups/CU x 4
     first at ViT-L/32 size and 4 x 1 at ResNet-101 size on one box (bench.py
     aux_kernels.posterior_sample.mix_ceiling, profiles/round4/methods/), and
-    round 2's probes ranked 2 x 4 first on two others."""
+    round 2's probes ranked 2 x 4 first on two others; in round 4's
+    same-process A/Bs on ViT-L/32 draws 1 x 4 ran 0.587-0.600 ms against
+    0.635-0.653 for the best of the others on three boxes
+    (profiles/round4/philox_ab/)."""
     stream = L.current_stream_handle(out.device)
     best = None
     for bpc, u in SAMPLE_GEOMETRIES:

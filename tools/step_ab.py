@@ -33,7 +33,8 @@ def use(path):
     L.lib()
 
 
-METHOD = os.environ.get("METHOD", "csghmc")  # or "adam" (Adam-SGHMC + SGD), "sgld" (+ SGD)
+METHOD = os.environ.get("METHOD", "csghmc")  # or "adam" (Adam-SGHMC + SGD), "sgld" (+ SGD),
+# "draw" (the Welford posterior draw; GEOMS entries = workgroups/CU, unroll)
 use(libs[0])
 segs, readout = segments(os.environ.get("BACKBONE", "vit_l_32"), 1000)
 adam = METHOD == "adam"
@@ -55,6 +56,10 @@ lrs, alpha, N = (1e-4, 1e-2), 0.18, 1840.0
 
 
 def explore(i):
+    if METHOD == "draw":  # methods/csghmc.py:466-468 (mom1 = mean, mom2 = M2)
+        K.posterior_sample(st.mom, m1, m2, var_mode=L.VAR_WELFORD, ratio=1.0 / 7.0, seed=3,
+                           step=i, geometry=geoms_now[0][:2])
+        return
     if sgld:  # methods/sgld.py:469-484 + SGD(momentum 0.5), Philox
         K.sgmcmc_step(st, L.SGLD, lrs=lrs, noise_scale=(1e-3, 1e-3), noise_mode=L.NOISE_PHILOX,
                       prior_sig=1.0, sigma2=1.0, n_data=N * 1e3, mu=0.5, momentum=True,
@@ -95,16 +100,18 @@ def t(fn, reps=20):
     return e0.elapsed_time(e1) / reps
 
 
-res = {}
+res, geoms_now = {}, []
+m2.normal_(0.0, 1e-2, generator=gen).square_()
 for r in range(rounds):
     for path in libs:
         use(path)
         for g in geoms:
+            geoms_now[:] = [g]
             K.set_launch_config(*g)
-            for name, fn, bpe in (("adam" if adam else "sgld" if sgld else "explore", explore,
-                                   48 if adam else 24 if sgld else 20),
+            for name, fn, bpe in ((METHOD if METHOD in ("adam", "sgld", "draw") else "explore",
+                                   explore, {"adam": 48, "sgld": 24, "draw": 12}.get(METHOD, 20)),
                                   ("collect", collect, 40 if sgld else 36)):
-                if name == "collect" and (g != geoms[0] or adam):
+                if name == "collect" and (g != geoms[0] or adam or METHOD == "draw"):
                     continue
                 ms = t(fn)
                 res.setdefault((os.path.basename(path), g, name), []).append(ms)
