@@ -564,6 +564,13 @@ int check_runs_and_grad(const bdl_step_args* s, const char* what) {
   return BDL_OK;
 }
 
+// Graph-node binding (bdl_graph_last_node / bdl_graph_redirect): the kernel
+// node the thread's last captured step launch added, and the instantiated
+// graph + node its next step launches rewrite instead of launching.
+thread_local hipGraphNode_t g_captured_node = nullptr;
+thread_local hipGraphExec_t g_redirect_exec = nullptr;
+thread_local hipGraphNode_t g_redirect_node = nullptr;
+
 int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   if (!s) return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: null args");
   if (s->n < 0) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: n < 0");
@@ -645,12 +652,40 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   a.inv_ca = recip_or(s->inv_collect_a, s->collect_a);
   a.inv_cb = recip_or(s->inv_collect_b, s->collect_b);
 
+  if (g_redirect_exec) {
+    void* kp[] = {&a};
+    hipKernelNodeParams p{};
+    p.func = (void*)k;
+    p.gridDim = dim3((unsigned)grid);
+    p.blockDim = dim3(kBlock);
+    p.sharedMemBytes = (unsigned)run_lds_bytes(s);
+    p.kernelParams = kp;
+    const hipError_t err = hipGraphExecKernelNodeSetParams(g_redirect_exec, g_redirect_node, &p);
+    if (err != hipSuccess) {
+      (void)hipGetLastError();
+      g_last_error = std::string("bdl_sgmcmc_step: graph node update failed: ") +
+                     hipGetErrorString(err);
+      return BDL_ERR_LAUNCH;
+    }
+    return BDL_OK;
+  }
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kBlock), run_lds_bytes(s), stream, a);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     g_last_error = std::string("bdl_sgmcmc_step: launch failed: ") + hipGetErrorString(err);
     return BDL_ERR_LAUNCH;
   }
+  g_captured_node = nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (stream && hipStreamIsCapturing(stream, &cs) == hipSuccess &&
+      cs == hipStreamCaptureStatusActive) {
+    const hipGraphNode_t* deps = nullptr;
+    size_t ndeps = 0;
+    if (hipStreamGetCaptureInfo_v2(stream, &cs, nullptr, nullptr, &deps, &ndeps) == hipSuccess &&
+        ndeps == 1)
+      g_captured_node = deps[0];
+  }
+  (void)hipGetLastError();
   return BDL_OK;
 }
 
@@ -737,6 +772,19 @@ using namespace bdl;
 extern "C" {
 
 int bdl_version(void) { return BDL_ABI_VERSION; }
+
+int bdl_graph_last_node(void** node) {
+  if (!node) return fail(BDL_ERR_NULL, "bdl_graph_last_node: null out pointer");
+  *node = (void*)g_captured_node;
+  return BDL_OK;
+}
+
+int bdl_graph_redirect(void* graph_exec, void* node) {
+  if (graph_exec && !node) return fail(BDL_ERR_NULL, "bdl_graph_redirect: null node");
+  g_redirect_exec = (hipGraphExec_t)graph_exec;
+  g_redirect_node = graph_exec ? (hipGraphNode_t)node : nullptr;
+  return BDL_OK;
+}
 
 const char* bdl_last_error(void) { return g_last_error.c_str(); }
 
