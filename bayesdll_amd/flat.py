@@ -544,7 +544,9 @@ class FlatState:
         tab = self._grad_tables.get(key) if deferred is None else None
         if tab is None:
             nt = len(idx)
-            host = torch.empty(3 * nt, dtype=torch.int64).pin_memory()
+            host = torch.empty(3 * nt, dtype=torch.int64)
+            if deferred is None:  # (no pinned allocation inside a capture)
+                host = host.pin_memory()
             h = host.numpy()
             for j, (i, ptr) in enumerate(zip(idx, ptrs)):
                 o, k = self.offsets[i], self.numels[i]

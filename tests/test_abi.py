@@ -455,7 +455,8 @@ def test_integration_snippet_is_the_tested_reference_binding():
     _, path = _reference_binding()
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     assert open(path).read() in doc
-    assert "ABI version 6" in doc and "ABI version 5" not in doc
+    from bayesdll_amd import _lib as L
+    assert f"ABI version {L.ABI_VERSION}" in doc and f"ABI version {L.ABI_VERSION - 1}" not in doc
 
 
 def test_reference_binding_struct_matches_header_and_library():
