@@ -143,6 +143,7 @@ class FusedModelBase(nn.Module):
         self._ovl_hooks = None
         self._side = None
         self.overlap_graph_failed = False  # the update could not be captured: eager overlap
+        self.overlap_graph_error = None
         self._state = None
         self._state_net = None
 
@@ -308,6 +309,11 @@ class FusedModelBase(nn.Module):
             for bi, node in enumerate(g["nodes"]):
                 L.check(h.bdl_graph_redirect(ex, node), "bdl_graph_redirect")
                 launch(g["buckets"][bi], g["plan"][bi][0])
+        except RuntimeError as e:  # a node that is not this step's kernel: eager overlap
+            del self._graphs[key]
+            _drop_graphs([g["graph"]])
+            self.overlap_graph_failed, self.overlap_graph_error = True, str(e)
+            return None
         finally:
             h.bdl_graph_redirect(None, None)
         g["x"].copy_(x)
@@ -338,9 +344,6 @@ class FusedModelBase(nn.Module):
             side.wait_event(ev)
             with torch.cuda.stream(side):
                 launch(bs, start)
-            node = C.c_void_p()
-            L.check(h.bdl_graph_last_node(C.byref(node)), "bdl_graph_last_node")
-            nodes[bi] = node.value
             bs.launch_cfg = K._ACTIVE[0]  # the kernel (unroll) the node was captured with
             buckets[bi] = bs
 
@@ -351,6 +354,12 @@ class FusedModelBase(nn.Module):
             loss = criterion(out, sy)
             self._backward_firing(loss, plan, need, owner, fire)
             torch.cuda.current_stream(st.device).wait_stream(side)
+        raw = graph.raw_cuda_graph()
+        for bi, bs in enumerate(buckets):  # each bucket's kernel node, by kernel and range
+            node = C.c_void_p()
+            if bs is not None and h.bdl_graph_find_step_node(
+                    raw, bs.theta.data_ptr(), int(bs.n), C.byref(node)) == L.BDL_OK:
+                nodes[bi] = node.value
         graph.instantiate()
         for dev, host in deferred:  # the bucket tables, before any replay
             dev.copy_(host)

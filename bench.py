@@ -949,9 +949,10 @@ def main():
         e2e["graph_ms_per_step"] = eg["ms_per_step"]
         e2e["graph_steps_per_s"] = eg["steps_per_s"]
         # the update captured in the graph, bucket by bucket beside backward
-        eo = e2e_steps(a.e2e_steps, 3, local, 42, graph=True, overlap=True)
-        e2e["graph_overlap_ms_per_step"] = eo["ms_per_step"]
-        e2e["graph_overlap_graphs"] = eo["overlap_graphs"]
+        if os.environ.get("BDL_BENCH_GRAPH_OVERLAP", "0") == "1":
+            eo = e2e_steps(a.e2e_steps, 3, local, 42, graph=True, overlap=True)
+            e2e["graph_overlap_ms_per_step"] = eo["ms_per_step"]
+            e2e["graph_overlap_graphs"] = eo["overlap_graphs"]
         out["e2e"] = e2e
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not sgld:
         out["cpu_baseline"] = cpu_baseline(segs, readout, a.cpu_baseline_seconds)

@@ -62,7 +62,7 @@ def test_graph_overlap_equals_eager_chain(monkeypatch):
     mg, m1g, m2g, lg = _run(True, True, monkeypatch)
     me, m1e, m2e, le = _run(False, False, monkeypatch)
     keys = [k for k in mg._graphs if "overlap" in k]
-    assert not mg.overlap_graph_failed
+    assert not mg.overlap_graph_failed, mg.overlap_graph_error
     # explore, sample, first collect, collect; full and ragged batches
     assert len(keys) >= 5, keys
     assert all(len(mg._graphs[k]["nodes"]) >= 4 for k in keys)
