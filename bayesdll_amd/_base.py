@@ -21,7 +21,6 @@ Noise modes (`Model.noise_mode`, or env BDL_NOISE_MODE):
 from __future__ import annotations
 
 import contextlib
-import ctypes as C
 import gc
 import os
 
@@ -60,7 +59,6 @@ def _drop_graphs(graphs):
         graphs.clear()
         release_deferred_graphs()
 MAX_GRAPHS = 4  # captured forward/backward graphs per sampler (one per input shape)
-MAX_OVERLAP_GRAPHS = 16  # with the update captured: one per (input shape, step kind)
 
 
 @contextlib.contextmanager
@@ -142,8 +140,6 @@ class FusedModelBase(nn.Module):
         self._ovl_plan = None
         self._ovl_hooks = None
         self._side = None
-        self.overlap_graph_failed = False  # the update could not be captured: eager overlap
-        self.overlap_graph_error = None
         self._state = None
         self._state_net = None
 
@@ -190,9 +186,10 @@ class FusedModelBase(nn.Module):
         return loss, out
 
     def can_overlap(self, st):
-        return self.overlap and st.grad_mode == "tensor" and self.noise_mode == "philox"
+        return (self.overlap and not self.graph and st.grad_mode == "tensor"
+                and self.noise_mode == "philox")
 
-    def forward_backward_overlapped(self, st, net, x, y, criterion, launch, kind=None):
+    def forward_backward_overlapped(self, st, net, x, y, criterion, launch):
         """Forward + backward with the fused update overlapped: the flat
         vectors are cut into ~64 MB buckets of whole tensors
         (FlatState.bucket_plan); when the last gradient of a bucket has been
@@ -204,51 +201,7 @@ class FusedModelBase(nn.Module):
         and (with philox_offset = start // 4) the same noise as one launch:
         the chain is bit-identical.  Buckets holding a parameter without a
         gradient are launched after backward, with it skipped.  Philox noise
-        and "tensor" gradients only (can_overlap).  In graph mode the bucket
-        launches are captured with forward and backward, one graph per `kind`
-        (the step's kernel selection), _graphed_overlapped."""
-        if self.graph and kind is not None and x.is_cuda and y.is_cuda and \
-                torch.is_grad_enabled():
-            got = self._graphed_overlapped(st, net, x, y, criterion, launch, kind)
-            if got is not None:
-                return got
-        self._ensure_ovl_plan(st)
-        _, plan, owner, need = self._ovl_plan
-        main = torch.cuda.current_stream(st.device)
-        side = self._side
-
-        def fire(bi):
-            start, end, idx = plan[bi]
-            ptrs = [0 if st.params[i].grad is None else st.params[i].grad.data_ptr() for i in idx]
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                launch(st.bucket_state(plan[bi], ptrs), start)
-
-        out = net(x)
-        loss = criterion(out, y)
-        st.zero_grad()
-        self._backward_firing(loss, plan, need, owner, fire)
-        main.wait_stream(side)
-        st.sync_grads()  # which parameters got a gradient (has_grad / noise bookkeeping)
-        return loss, out
-
-    def _backward_firing(self, loss, plan, need, owner, fire):
-        """loss.backward() with each bucket's `fire` called from the hook of
-        its last gradient; buckets not fired by then are fired after it."""
-        self._ovl = {"pending": list(need), "done": [False] * len(plan), "fire": fire,
-                     "owner": owner}
-        try:
-            loss.backward()
-        finally:
-            ctx, self._ovl = self._ovl, None
-        for bi, d in enumerate(ctx["done"]):
-            if not d:
-                ctx["done"][bi] = True
-                fire(bi)
-
-    def _ensure_ovl_plan(self, st):
+        and "tensor" gradients only (can_overlap)."""
         dev = st.device
         if self._ovl_plan is None or self._ovl_plan[0] is not st:
             plan = st.bucket_plan(OVERLAP_BUCKET_ELEMS)
@@ -264,6 +217,35 @@ class FusedModelBase(nn.Module):
             self._ovl_hooks = [p.register_post_accumulate_grad_hook(self._ovl_hook(i))
                                for i, p in enumerate(st.params) if st.requires_grad[i]]
             self._side = torch.cuda.Stream(dev)
+        _, plan, owner, need = self._ovl_plan
+        main = torch.cuda.current_stream(dev)
+        side = self._side
+
+        def fire(bi):
+            start, end, idx = plan[bi]
+            ptrs = [0 if st.params[i].grad is None else st.params[i].grad.data_ptr() for i in idx]
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                launch(st.bucket_state(plan[bi], ptrs), start)
+
+        out = net(x)
+        loss = criterion(out, y)
+        st.zero_grad()
+        self._ovl = {"pending": list(need), "done": [False] * len(plan), "fire": fire,
+                     "owner": owner}
+        try:
+            loss.backward()
+        finally:
+            ctx, self._ovl = self._ovl, None
+        for bi, d in enumerate(ctx["done"]):
+            if not d:
+                ctx["done"][bi] = True
+                fire(bi)
+        main.wait_stream(side)
+        st.sync_grads()  # which parameters got a gradient (has_grad / noise bookkeeping)
+        return loss, out
 
     def _ovl_hook(self, i):
         def hook(_p):
@@ -276,111 +258,6 @@ class FusedModelBase(nn.Module):
                 ctx["done"][bi] = True
                 ctx["fire"](bi)
         return hook
-
-    def _graphed_overlapped(self, st, net, x, y, criterion, launch, kind):
-        """Graph mode with the update inside the graph, overlapped with the
-        backward: the bucket launches of forward_backward_overlapped are
-        captured on the side stream (fork / join through events), so the
-        memory-bound sweep of a bucket runs beside the GEMM-bound backward of
-        the layers below it.  The step's scalars change every step (learning
-        rate, noise scale, Philox step, moment vectors, counts): before each
-        replay every bucket's kernel node is rewritten in the instantiated
-        graph (bdl_graph_redirect, hipGraphExecKernelNodeSetParams) by the
-        same `launch` call the eager path makes, so the arguments are formed
-        by one code path.  One graph per (input shape, kind), `kind` naming
-        the kernel the step selects (noise on / off, collect kind).  Same
-        kernels, same arguments, same order per bucket as eager: bit-identical
-        chains (tests/test_gpu_graph_overlap.py)."""
-        key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, net.training, id(criterion),
-               id(net), "overlap", kind)
-        g = self._graphs.get(key)
-        if g is None:
-            if len(self._graphs) >= MAX_OVERLAP_GRAPHS:
-                return None
-            g = self._capture_overlapped(st, net, x, y, criterion, launch)
-            if g is None:
-                self.overlap_graph_failed = True
-                return None
-            self._graphs[key] = g
-        self._bind_graph_grads(st, g)
-        h = L.lib()
-        ex = g["graph"].raw_cuda_graph_exec()
-        try:
-            for bi, node in enumerate(g["nodes"]):
-                L.check(h.bdl_graph_redirect(ex, node), "bdl_graph_redirect")
-                launch(g["buckets"][bi], g["plan"][bi][0])
-        except RuntimeError as e:  # a node that is not this step's kernel: eager overlap
-            del self._graphs[key]
-            _drop_graphs([g["graph"]])
-            self.overlap_graph_failed, self.overlap_graph_error = True, str(e)
-            return None
-        finally:
-            h.bdl_graph_redirect(None, None)
-        g["x"].copy_(x)
-        g["y"].copy_(y)
-        g["graph"].replay()
-        st.use_grad_table(g["table"])
-        if st._touched:
-            st._touched[:] = g["touched"]
-        return g["loss"], g["out"].detach().clone()
-
-    def _capture_overlapped(self, st, net, x, y, criterion, launch):
-        from . import kernels as K
-        sx, sy = x.detach().clone(), y.detach().clone()
-        self._warm_up(st, net, sx, sy, criterion)
-        self._ensure_ovl_plan(st)
-        _, plan, owner, need = self._ovl_plan
-        side = self._side
-        nodes, buckets, deferred = [None] * len(plan), [None] * len(plan), []
-        h = L.lib()
-
-        def fire(bi):
-            start, end, idx = plan[bi]
-            ptrs = [0 if st.params[i].grad is None else st.params[i].grad.data_ptr() for i in idx]
-            bs = st.bucket_state(plan[bi], ptrs, deferred=deferred)
-            main = torch.cuda.current_stream(st.device)
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                launch(bs, start)
-            bs.launch_cfg = K._ACTIVE[0]  # the kernel (unroll) the node was captured with
-            buckets[bi] = bs
-
-        st.zero_grad()
-        graph = torch.cuda.CUDAGraph(keep_graph=True)  # node handles stay valid
-        with no_gc(), torch.cuda.graph(graph):
-            out = net(sx)
-            loss = criterion(out, sy)
-            self._backward_firing(loss, plan, need, owner, fire)
-            torch.cuda.current_stream(st.device).wait_stream(side)
-        raw = graph.raw_cuda_graph()
-        for bi, bs in enumerate(buckets):  # each bucket's kernel node, by kernel and range
-            node = C.c_void_p()
-            if bs is not None and h.bdl_graph_find_step_node(
-                    raw, bs.theta.data_ptr(), int(bs.n), C.byref(node)) == L.BDL_OK:
-                nodes[bi] = node.value
-        graph.instantiate()
-        for dev, host in deferred:  # the bucket tables, before any replay
-            dev.copy_(host)
-        if any(n is None for n in nodes) or any(
-                p.grad is not None and (p.grad.dtype != torch.float32 or
-                                        not p.grad.is_contiguous()) for p in st.params):
-            _drop_graphs([graph])
-            return None
-        st.sync_grads()
-        out, loss = out.detach(), loss.detach()
-        self.graph_captures += 1
-        return {"graph": graph, "x": sx, "y": sy, "out": out, "loss": loss,
-                "grads": [p.grad for p in st.params], "touched": list(st._touched),
-                "table": st.grad_table(), "nodes": nodes, "buckets": buckets, "plan": plan}
-
-    def _bind_graph_grads(self, st, g):
-        if g is not self._graph_bound or any(p.grad is not gt
-                                             for p, gt in zip(st.params, g["grads"])):
-            for p, gt in zip(st.params, g["grads"]):
-                p.grad = gt
-        self._graph_bound = g
 
     def _graphed_forward_backward(self, st, net, x, y, criterion):
         """Forward + loss + backward replayed from a captured HIP graph
@@ -408,11 +285,15 @@ class FusedModelBase(nn.Module):
                 self.graph = False
                 return None
             self._graphs[key] = g
-        # another shape's graph (a ragged last batch, then the next epoch's
-        # full one), an eager step or user code left other tensors in .grad:
-        # point every .grad at this graph's static gradient outputs (the
-        # update reads them through the graph's table either way)
-        self._bind_graph_grads(st, g)
+        if g is not self._graph_bound or any(p.grad is not gt
+                                             for p, gt in zip(st.params, g["grads"])):
+            # another shape's graph (a ragged last batch, then the next epoch's
+            # full one), an eager step or user code left other tensors in .grad:
+            # point every .grad at this graph's static gradient outputs (the
+            # update reads them through the graph's table either way)
+            for p, gt in zip(st.params, g["grads"]):
+                p.grad = gt
+        self._graph_bound = g
         g["x"].copy_(x)
         g["y"].copy_(y)
         g["graph"].replay()
@@ -443,7 +324,24 @@ class FusedModelBase(nn.Module):
 
     def _capture(self, st, net, x, y, criterion):
         sx, sy = x.detach().clone(), y.detach().clone()
-        self._warm_up(st, net, sx, sy, criterion)
+        gc.collect()  # pending garbage (old pools included) goes before the capture, not in it
+        release_deferred_graphs()
+        # warm-up passes on a side stream (library handles, autotuned kernels)
+        # must not move the network's state: keep buffers (BatchNorm running
+        # statistics) and the device RNG as they were
+        bufs = [b.detach().clone() for b in net.buffers()]
+        rng = torch.cuda.get_rng_state(st.device)
+        side = torch.cuda.Stream(st.device)
+        side.wait_stream(torch.cuda.current_stream(st.device))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                st.zero_grad()
+                criterion(net(sx), sy).backward()
+        torch.cuda.current_stream(st.device).wait_stream(side)
+        with torch.no_grad():
+            for b, c in zip(net.buffers(), bufs):
+                b.copy_(c)
+        torch.cuda.set_rng_state(rng, st.device)
         st.zero_grad()  # "tensor" mode: .grad = None, so the graph's gradients are its own
         graph = torch.cuda.CUDAGraph()
         with no_gc(), torch.cuda.graph(graph):
@@ -465,26 +363,6 @@ class FusedModelBase(nn.Module):
         return {"graph": graph, "x": sx, "y": sy, "out": out, "loss": loss,
                 "grads": [p.grad for p in st.params], "touched": list(st._touched),
                 "table": st.grad_table()}
-
-    def _warm_up(self, st, net, sx, sy, criterion):
-        gc.collect()  # pending garbage (old pools included) goes before the capture, not in it
-        release_deferred_graphs()
-        # warm-up passes on a side stream (library handles, autotuned kernels)
-        # must not move the network's state: keep buffers (BatchNorm running
-        # statistics) and the device RNG as they were
-        bufs = [b.detach().clone() for b in net.buffers()]
-        rng = torch.cuda.get_rng_state(st.device)
-        side = torch.cuda.Stream(st.device)
-        side.wait_stream(torch.cuda.current_stream(st.device))
-        with torch.cuda.stream(side):
-            for _ in range(2):
-                st.zero_grad()
-                criterion(net(sx), sy).backward()
-        torch.cuda.current_stream(st.device).wait_stream(side)
-        with torch.no_grad():
-            for b, c in zip(net.buffers(), bufs):
-                b.copy_(c)
-        torch.cuda.set_rng_state(rng, st.device)
 
     # -------------------------------------------------------------- noise
     def draw_noise(self, st):

@@ -98,9 +98,6 @@ EXPORTS = {
     "bdl_philox_normal": (C.c_int, [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint64,
                                     C.c_void_p]),
     "bdl_set_launch_config": (C.c_int, [C.c_int32, C.c_int32, C.c_int32]),
-    "bdl_graph_find_step_node": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64,
-                                            C.POINTER(C.c_void_p)]),
-    "bdl_graph_redirect": (C.c_int, [C.c_void_p, C.c_void_p]),
     # include/bdl_placement.h
     "bdl_chunk_granularity": (C.c_int, [C.c_int32, C.POINTER(C.c_uint64)]),
     "bdl_chunk_create": (C.c_int, [C.c_int32, C.c_uint64, C.POINTER(C.c_uint64)]),

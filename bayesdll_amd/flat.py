@@ -528,25 +528,19 @@ class FlatState:
             out.append((start, self.n, tuple(cur)))
         return out
 
-    def bucket_state(self, bucket, ptrs, deferred=None):
+    def bucket_state(self, bucket, ptrs):
         """A launchable view of one bucket: every vector sliced to
         [start, end), a per-tensor run table with ends relative to `start`
         and gradient bases shifted so local element e reads
         ptrs[j] + 4*(start + e - offset_j); launch it with
-        philox_offset = start // 4 for the whole-vector noise.  deferred: a
-        list, inside a HIP-graph capture: the table is allocated but not
-        filled (a copy captured from pinned memory would be replayed from a
-        buffer that has since been freed); (device table, pinned host table)
-        is appended for the caller to copy once the capture has ended."""
+        philox_offset = start // 4 for the whole-vector noise."""
         from types import SimpleNamespace
         start, end, idx = bucket
         key = (start, tuple(ptrs))
-        tab = self._grad_tables.get(key) if deferred is None else None
+        tab = self._grad_tables.get(key)
         if tab is None:
             nt = len(idx)
-            host = torch.empty(3 * nt, dtype=torch.int64)
-            if deferred is None:  # (no pinned allocation inside a capture)
-                host = host.pin_memory()
+            host = torch.empty(3 * nt, dtype=torch.int64).pin_memory()
             h = host.numpy()
             for j, (i, ptr) in enumerate(zip(idx, ptrs)):
                 o, k = self.offsets[i], self.numels[i]
@@ -555,16 +549,11 @@ class FlatState:
                 if ptr and base % 16:
                     at |= L.ATTR_GUNALIGNED
                 h[2 * j], h[2 * j + 1], h[2 * nt + j] = o + k - start, at, base
-            if deferred is None:
-                dev = host.to(self.device, non_blocking=True)
-            else:
-                dev = torch.empty(3 * nt, dtype=torch.int64, device=self.device)
-                deferred.append((dev, host))
+            dev = host.to(self.device, non_blocking=True)
             tab = (dev[:2 * nt].view(nt, 2), nt, dev[2 * nt:])
-            if deferred is None:
-                if len(self._grad_tables) >= 4 * GRAD_TABLE_CACHE:
-                    self._grad_tables.pop(next(iter(self._grad_tables)))
-                self._grad_tables[key] = tab
+            if len(self._grad_tables) >= 4 * GRAD_TABLE_CACHE:
+                self._grad_tables.pop(next(iter(self._grad_tables)))
+            self._grad_tables[key] = tab
         sl = (lambda v: None if v is None else v[start:end])
         return SimpleNamespace(theta=self.theta[start:end], grad=None, gbase=tab[2], runs=tab[0],
                                nruns=tab[1], mom=sl(self.mom), prior=sl(self.prior), noise=None,
