@@ -44,8 +44,6 @@ def release_deferred_graphs():
     if _DEFERRED_GRAPHS and not torch.cuda.is_current_stream_capturing():
         torch.cuda.synchronize()
         _DEFERRED_GRAPHS.clear()
-    from . import placement
-    placement.release_pending()  # chunk mappings whose last tensor died inside a capture
 
 
 def _drop_graphs(graphs):
@@ -112,7 +110,7 @@ class FusedModelBase(nn.Module):
     need_prior = False
     need_mom = True
     tune_method = "sgld"  # which production kernel autotune_once times for this sampler
-    extra_vectors = ()    # further per-element state placed with the chain (FlatState.extra)
+    extra_vectors = ()    # further per-element state of the chain (FlatState.extra)
 
     # set by the bundled Runners: Model.forward returns the loss as a device
     # scalar instead of loss.item(), so a step issues no host synchronisation
@@ -154,7 +152,7 @@ class FusedModelBase(nn.Module):
                                     bias=getattr(self, "bias", "informative"),
                                     need_prior=self.need_prior, need_mom=self.need_mom,
                                     need_noise=self.noise_mode != "philox",
-                                    placement=self.tune_method, extra=self.extra_vectors)
+                                    extra=self.extra_vectors)
             self._state_net = net
             steps_timed = int(os.environ.get("BDL_STEP_TIMING", "0") or 0)
             if steps_timed > 0:  # sampled update timing, logged once per epoch

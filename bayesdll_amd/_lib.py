@@ -23,9 +23,8 @@ NOISE_NONE, NOISE_BUFFER, NOISE_PHILOX = 0, 1, 2
 COLLECT_NONE, COLLECT_WELFORD_INIT, COLLECT_WELFORD, COLLECT_MEAN_INIT, COLLECT_MEAN = range(5)
 ATTR_HEAD, ATTR_PRIOR, ATTR_SKIP, ATTR_GUNALIGNED = 0x1, 0x2, 0x4, 0x8
 FLAG_FIRST_STEP, FLAG_RECIP_DIV, FLAG_MOMENTUM, FLAG_GRAD_READY = 0x1, 0x2, 0x4, 0x8
-FLAG_PLACEMENT_PROBE = 0x10
 VAR_GIVEN, VAR_RAW_MOMENTS, VAR_WELFORD = 0, 1, 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _fp = C.c_void_p
 
@@ -64,8 +63,7 @@ class AdamArgs(C.Structure):
                 ("bias_corr2", C.c_float), ("eps", C.c_float), ("two_alpha", C.c_float),
                 ("nd", C.c_float), ("temperature", C.c_float), ("inv_bias_corr1", C.c_float),
                 ("inv_bias_corr2", C.c_float), ("inv_temperature", C.c_float),
-                ("pad2", C.c_float), ("grad_is_mom", C.c_int32), ("tile_log2", C.c_int32),
-                ("tile_streams", C.c_int32), ("tile_mask", C.c_uint32)]
+                ("pad2", C.c_float), ("grad_is_mom", C.c_int32)]
 
 
 class MomentsArgs(C.Structure):
@@ -98,14 +96,7 @@ EXPORTS = {
     "bdl_philox_normal": (C.c_int, [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint64,
                                     C.c_void_p]),
     "bdl_set_launch_config": (C.c_int, [C.c_int32, C.c_int32, C.c_int32]),
-    # include/bdl_placement.h
-    "bdl_chunk_granularity": (C.c_int, [C.c_int32, C.POINTER(C.c_uint64)]),
-    "bdl_chunk_create": (C.c_int, [C.c_int32, C.c_uint64, C.POINTER(C.c_uint64)]),
-    "bdl_chunk_release": (C.c_int, [C.c_uint64]),
-    "bdl_vmm_map": (C.c_int, [C.c_int32, C.POINTER(C.c_uint64), C.c_int32, C.c_uint64,
-                              C.POINTER(C.c_void_p)]),
-    "bdl_vmm_unmap": (C.c_int, [C.c_void_p, C.c_uint64]),
-    "bdl_vmm_arena_info": (C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    # include/bdl_measure.h
     "bdl_stream_mix": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.POINTER(C.c_void_p),
                                  C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_void_p]),
 }

@@ -25,7 +25,7 @@ import torch.nn.functional as F
 from . import _lib as L
 from . import chains
 from . import kernels as K
-from .flat import bind_parameters, draw_buffer, fill_normal_per_tensor
+from .flat import bind_parameters, fill_normal_per_tensor
 
 EVAL_STEP_BASE = 1 << 62  # Philox step keys for evaluation draws (never used by training)
 
@@ -45,26 +45,8 @@ class PosteriorDraw:
         self.count = 0
         self.noise = None if noise_mode == "philox" else torch.empty_like(self.theta)
         self.provider = provider
-        self.placement = None  # draw_buffer's info ({} when it placed nothing), once a Philox draw placed theta
         if noise_mode == "external" and provider is None:
             raise RuntimeError("noise_mode='external' needs Model.noise_provider")
-
-    def _place(self, mean, m2, var_mode, ratio):
-        """Before the first Philox draw: time the draw into this copy's theta
-        and into fresh allocations, and rebind the network to the fastest
-        (flat.draw_buffer).  The timing launches use this draw's own keys, so
-        they change no result."""
-        step = EVAL_STEP_BASE + self.count
-
-        def launch(buf, off=0):
-            m = buf.numel()
-            K.posterior_sample(buf, mean[off:off + m], None if m2 is None else m2[off:off + m],
-                               var_mode=var_mode, ratio=ratio, seed=self.seed, chain=self.chain,
-                               step=step)
-        buf, info = draw_buffer(self.theta, launch)
-        self.placement = info or {}
-        if buf is not self.theta:
-            self.theta = bind_parameters(self.net, buf)
 
     def load_mean(self, mean):
         self.theta.copy_(mean)
@@ -72,9 +54,6 @@ class PosteriorDraw:
     def draw(self, mean, m2, var_mode, ratio):
         """theta = mean + sqrt(clamp(var, 1e-12)) * eps; m2=None -> var = 1e-12."""
         noise = None
-        if self.placement is None and self.noise_mode == "philox" and not \
-                torch.cuda.is_current_stream_capturing():
-            self._place(mean, m2, var_mode, ratio)
         if self.noise_mode == "torch":
             noise = fill_normal_per_tensor(self.noise, self.numels)
         elif self.noise_mode == "external":

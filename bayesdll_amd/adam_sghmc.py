@@ -61,7 +61,7 @@ class Model(FusedModelBase):
     need_prior = True
     need_mom = True   # v_mom (the reference's momentum_buffer)
     tune_method = "adam"
-    extra_vectors = K.ADAM_EXTRA  # adam_m, adam_v, sgd_buf: placed with theta / v_mom
+    extra_vectors = K.ADAM_EXTRA  # adam_m, adam_v, sgd_buf
     grad_is_mom = False
 
     def __init__(self, ND, prior_sig=1.0, bias="informative", momentum_decay=0.05, beta1=0.9,

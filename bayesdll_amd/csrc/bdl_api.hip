@@ -33,10 +33,7 @@
 // method, compiled in parallel), this file (host entry points of the C-ABI,
 // validation, launch geometry, the clip-norm / moments / sample kernels).
 #include "bdl_kernels.hpp"
-#include "bdl_placement.h"
-
-#include <mutex>
-#include <vector>
+#include "bdl_measure.h"
 
 namespace bdl {
 namespace {
@@ -164,7 +161,7 @@ __device__ __forceinline__ void sqnorm_body(const KArgs& a, double* __restrict__
           while (rr < a.nruns - 1 && run_end(rr) <= e + j) ++rr;
           const uint32_t at = run_attr(rr);
           if (at & BDL_ATTR_SKIP) continue;  // .grad is None: not in the norm
-          float xt = th[j], xg = gt ? run_grad(a, rr)[e + j] : g[j], xv = 0.f;
+          float xt = th[j], xg = gt ? sload(run_grad(a, rr) + e + j) : g[j], xv = 0.f;
           const float ns = (at & BDL_ATTR_HEAD) ? a.ns1 : a.ns0;
           if (at & BDL_ATTR_PRIOR)
             update_core<BDL_SGLD_GRAD, NOISE, RECIP, true, false>(a, c, 0.f, ns, xt, xg, xv, t0[j], ep[j]);
@@ -496,32 +493,6 @@ StepKernel pick_step(int method, int noise, int collect, int unroll) {
   return nullptr;
 }
 
-// Placement probe (BDL_FLAG_PLACEMENT_PROBE): the production update under its
-// own symbol, so that the buffer-placement timing launches (flat.placed_vectors)
-// never mix into a kernel-trace summary of the production kernels.
-template <int METHOD, int NOISE, int COLLECT, int UNROLL>
-__global__ __launch_bounds__(kBlock) void bdl_probe_kernel(const KArgs a) {
-  if (a.flags & BDL_FLAG_RECIP_DIV)
-    step_body<METHOD, NOISE, COLLECT, true, UNROLL>(a);
-  else
-    step_body<METHOD, NOISE, COLLECT, false, UNROLL>(a);
-}
-
-StepKernel pick_probe(int method, int noise, int collect) {
-  if (collect != BDL_COLLECT_NONE) return nullptr;
-  if (method == BDL_CSGHMC && noise == BDL_NOISE_NONE)
-    return bdl_probe_kernel<BDL_CSGHMC, BDL_NOISE_NONE, BDL_COLLECT_NONE, 4>;
-  if (method == BDL_SGLD && noise == BDL_NOISE_PHILOX)
-    return bdl_probe_kernel<BDL_SGLD, BDL_NOISE_PHILOX, BDL_COLLECT_NONE, 4>;
-  return nullptr;
-}
-
-// A/B flavours only (make flavor D=-DBDL_GRID_PCT=75): the step grid as a
-// percentage of workgroups/CU x CUs
-#ifndef BDL_GRID_PCT
-#define BDL_GRID_PCT 100
-#endif
-
 int grid_for(int64_t ngroups, int per_block_groups) {
   const int64_t want = (ngroups + per_block_groups - 1) / per_block_groups;
   const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
@@ -594,15 +565,13 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   for (const void* p : ptrs)
     if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_sgmcmc_step: vector not 16-B aligned");
 
-  const bool probe = (s->flags & BDL_FLAG_PLACEMENT_PROBE) != 0;
-  const int unroll = probe ? 4 : g_unroll;
-  StepKernel k = probe ? pick_probe(s->method, s->noise_mode, s->collect)
-                       : pick_step(s->method, s->noise_mode, s->collect, unroll);
+  const int unroll = g_unroll;
+  StepKernel k = pick_step(s->method, s->noise_mode, s->collect, unroll);
   if (!k) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: unsupported method/noise/collect combination");
 
   const int64_t ngroups = (s->n + 3) / 4;
   const int64_t per_iter = (int64_t)kBlock * unroll;
-  const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu * BDL_GRID_PCT / 100;
+  const int64_t cap = (int64_t)device_cu_count() * g_blocks_per_cu;
   int64_t iters = (ngroups + per_iter - 1) / per_iter;
   int64_t grid = std::max<int64_t>(1, std::min(iters, cap));
   int64_t iters_per_block = (iters + grid - 1) / grid;
@@ -885,12 +854,6 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
     return fail(BDL_ERR_NULL, "bdl_adam_step: mom1 is required to collect");
   if (s->flags & BDL_FLAG_GRAD_READY)
     return fail(BDL_ERR_ARG, "bdl_adam_step: GRAD_READY is not an Adam flag (use bdl_sgmcmc_step)");
-  if (ad->tile_log2 < 0 || ad->tile_log2 > 40 || (ad->tile_log2 > 0 &&
-      (ad->tile_streams < 1 || ad->tile_streams > 4 || (ad->tile_mask & ~0xFu) || !ad->tile_mask)))
-    return fail(BDL_ERR_ARG, "bdl_adam_step: tile_log2 in [0, 40]; when tiled, tile_streams in "
-                "[1, 4] and tile_mask a non-empty subset of 0xF");
-  if (ad->tile_log2 > 0 && __builtin_popcount(ad->tile_mask) > ad->tile_streams)
-    return fail(BDL_ERR_ARG, "bdl_adam_step: tile_mask names more streams than tile_streams");
   const void* ptrs[] = {s->theta, s->mom, s->prior_mean, s->noise, s->mom1, s->mom2,
                         ad->adam_m, ad->adam_v, ad->sgd_buf};
   for (const void* p : ptrs)
@@ -929,9 +892,6 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
   a.adam_m = ad->adam_m;
   a.adam_v = ad->adam_v;
   a.sgd_buf = ad->sgd_buf;
-  a.tiled = ad->tile_log2 > 0 ? (int32_t)ad->tile_mask : 0;
-  a.tshift = ad->tile_log2;
-  a.tstride = ad->tile_log2 > 0 ? ((int64_t)ad->tile_streams << ad->tile_log2) : 0;
   a.b1 = ad->beta1;
   a.omb1 = ad->one_minus_beta1;
   a.b2 = ad->beta2;
@@ -1075,171 +1035,5 @@ int bdl_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t chain, uint
   return BDL_OK;
 }
 
-
-// ---------------------------------------------------------------------------
-// Physical-chunk placement (include/bdl_placement.h).  Host-only: hipMemCreate
-// physical chunks, mapped into contiguous virtual ranges with hipMemMap.  The
-// Python side (flat.placed_vectors) times chunk pairs with the production
-// kernel and maps theta / momentum from chunks that pair fast.
-static hipMemAllocationProp chunk_prop(int32_t device) {
-  hipMemAllocationProp prop;
-  memset(&prop, 0, sizeof prop);
-  prop.type = hipMemAllocationTypePinned;
-  prop.location.type = hipMemLocationTypeDevice;
-  prop.location.id = device;
-  return prop;
-}
-
-static int hip_fail(const char* what, hipError_t e) {
-  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
-  // clear the runtime's last error: the caller falls back to torch's
-  // allocator, whose next launch check would otherwise report this failure
-  (void)hipGetLastError();
-  return BDL_ERR_LAUNCH;
-}
-
-int bdl_chunk_granularity(int32_t device, uint64_t* bytes) {
-  if (!bytes) return fail(BDL_ERR_NULL, "bdl_chunk_granularity: null out");
-  hipMemAllocationProp prop = chunk_prop(device);
-  size_t g = 0;
-  const hipError_t e = hipMemGetAllocationGranularity(&g, &prop,
-                                                      hipMemAllocationGranularityRecommended);
-  if (e != hipSuccess) return hip_fail("bdl_chunk_granularity", e);
-  *bytes = g;
-  return BDL_OK;
-}
-
-int bdl_chunk_create(int32_t device, uint64_t bytes, uint64_t* handle) {
-  if (!handle) return fail(BDL_ERR_NULL, "bdl_chunk_create: null out");
-  if (bytes == 0) return fail(BDL_ERR_ARG, "bdl_chunk_create: zero bytes");
-  hipMemAllocationProp prop = chunk_prop(device);
-  hipMemGenericAllocationHandle_t h;
-  const hipError_t e = hipMemCreate(&h, bytes, &prop, 0);
-  if (e != hipSuccess) return hip_fail("bdl_chunk_create: hipMemCreate", e);
-  static_assert(sizeof(h) <= sizeof(uint64_t), "allocation handle wider than 64 bits");
-  uint64_t out = 0;
-  memcpy(&out, &h, sizeof h);
-  *handle = out;
-  return BDL_OK;
-}
-
-int bdl_chunk_release(uint64_t handle) {
-  hipMemGenericAllocationHandle_t h;
-  memcpy(&h, &handle, sizeof h);
-  const hipError_t e = hipMemRelease(h);
-  if (e != hipSuccess) return hip_fail("bdl_chunk_release: hipMemRelease", e);
-  return BDL_OK;
-}
-
-// Virtual-address arena.  Every mapping takes a fresh sub-range of a large
-// reservation made once (bump pointer, 2 MiB aligned), and no sub-range is
-// ever handed out twice: on this stack an address that has been mapped once
-// keeps translating to its first physical backing after hipMemUnmap (below),
-// and an address reserved with a null hint can be one that torch's allocator
-// used and freed (tools/vmm_alias_repro.cpp, scenario after_hipfree), so only
-// addresses from a range this library reserved up front and never reused are
-// known to be clean.  A new arena is reserved when one runs out.
-constexpr size_t kVmmAlign = (size_t)2 << 20;
-constexpr size_t kArenaBytes = (size_t)4 << 40;  // 4 TiB of address space per arena
-
-struct VmmArena {
-  char* base = nullptr;
-  size_t size = 0, used = 0;
-};
-std::mutex g_arena_mu;
-std::vector<VmmArena> g_arenas;
-size_t g_arena_mapped = 0;  // bytes of sub-ranges handed out so far
-
-static hipError_t arena_take(size_t bytes, void** out) {
-  std::lock_guard<std::mutex> lock(g_arena_mu);
-  const size_t need = (bytes + kVmmAlign - 1) / kVmmAlign * kVmmAlign;
-  if (g_arenas.empty() || g_arenas.back().used + need > g_arenas.back().size) {
-    hipError_t e = hipErrorOutOfMemory;
-    void* base = nullptr;
-    size_t size = std::max(kArenaBytes, need);
-    // a smaller arena if the driver refuses the large one
-    for (; size >= need; size /= 2) {
-      e = hipMemAddressReserve(&base, size, kVmmAlign, nullptr, 0);
-      if (e == hipSuccess) break;
-    }
-    if (e != hipSuccess) return e;
-    g_arenas.push_back(VmmArena{(char*)base, size, 0});
-  }
-  VmmArena& a = g_arenas.back();
-  *out = a.base + a.used;
-  a.used += need;
-  g_arena_mapped += need;
-  return hipSuccess;
-}
-
-int bdl_vmm_map(int32_t device, const uint64_t* handles, int32_t nchunks, uint64_t chunk_bytes,
-                void** va) {
-  if (!handles || !va) return fail(BDL_ERR_NULL, "bdl_vmm_map: null argument");
-  if (nchunks <= 0 || chunk_bytes == 0) return fail(BDL_ERR_ARG, "bdl_vmm_map: empty range");
-  if (chunk_bytes % kVmmAlign) return fail(BDL_ERR_ARG, "bdl_vmm_map: chunk_bytes not 2 MiB aligned");
-  const size_t total = (size_t)nchunks * (size_t)chunk_bytes;
-  void* base = nullptr;
-  hipError_t e = arena_take(total, &base);
-  if (e != hipSuccess) return hip_fail("bdl_vmm_map: hipMemAddressReserve", e);
-  int32_t mapped = 0;
-  for (; mapped < nchunks; ++mapped) {
-    hipMemGenericAllocationHandle_t h;
-    memcpy(&h, &handles[mapped], sizeof h);
-    e = hipMemMap((char*)base + (size_t)mapped * chunk_bytes, chunk_bytes, 0, h, 0);
-    if (e != hipSuccess) break;
-  }
-  if (e == hipSuccess) {
-    hipMemAccessDesc acc;
-    memset(&acc, 0, sizeof acc);
-    acc.location.type = hipMemLocationTypeDevice;
-    acc.location.id = device;
-    acc.flags = hipMemAccessFlagsProtReadWrite;
-    e = hipMemSetAccess(base, total, &acc, 1);
-    if (e == hipSuccess) {
-      *va = base;
-      return BDL_OK;
-    }
-  }
-  int rc;
-  {
-    std::lock_guard<std::mutex> lock(g_arena_mu);
-    char where[160];
-    snprintf(where, sizeof where,
-             "bdl_vmm_map: hipMemMap/hipMemSetAccess (arena %zu, offset %.1f of %.1f GiB)",
-             g_arenas.size(), (double)((char*)base - g_arenas.back().base) / 1073741824.0,
-             (double)g_arenas.back().size / 1073741824.0);
-    rc = hip_fail(where, e);
-  }
-  for (int32_t i = 0; i < mapped; ++i)
-    (void)hipMemUnmap((char*)base + (size_t)i * chunk_bytes, chunk_bytes);
-  // the sub-range is never handed out again (the bump pointer moved past it)
-  return rc;
-}
-
-int bdl_vmm_arena_info(uint64_t* reserved_bytes, uint64_t* mapped_bytes) {
-  std::lock_guard<std::mutex> lock(g_arena_mu);
-  uint64_t r = 0;
-  for (const VmmArena& a : g_arenas) r += a.size;
-  if (reserved_bytes) *reserved_bytes = r;
-  if (mapped_bytes) *mapped_bytes = g_arena_mapped;
-  return BDL_OK;
-}
-
-// The virtual sub-range stays taken after the unmap, for the life of the
-// process.  On this stack a virtual address that has been mapped once keeps
-// translating to its FIRST physical backing after hipMemUnmap: mapping other
-// chunks at that address — after hipMemAddressFree and a new reservation that
-// returns the same address, or re-mapping into the still-reserved range — sends
-// every write through the new mapping into the OLD chunks, with or without a
-// device synchronisation around the unmap and whether the range is unmapped
-// whole or chunk by chunk (tools/vmm_alias_repro.cpp, plain HIP, one scenario
-// per process: profiles/round3/vmm/).  Only a never-mapped address is correct,
-// so no sub-range of the arena is ever reused for other chunks.
-int bdl_vmm_unmap(void* va, uint64_t total_bytes) {
-  if (!va) return fail(BDL_ERR_NULL, "bdl_vmm_unmap: null va");
-  const hipError_t e = hipMemUnmap(va, total_bytes);
-  if (e != hipSuccess) return hip_fail("bdl_vmm_unmap: hipMemUnmap", e);
-  return BDL_OK;
-}
 
 }  // extern "C"

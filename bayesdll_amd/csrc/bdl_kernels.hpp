@@ -103,68 +103,32 @@ __device__ __forceinline__ f4v philox_normal4(uint64_t group, uint64_t seed, uin
 // Vector helpers: a 16-B "group" covers flat elements [4g, 4g+4).  Only the
 // very last group of a vector can be partial; it takes the guarded path.
 // ---------------------------------------------------------------------------
-// 16-B vector access.  Streaming (non-temporal) policy per direction:
-// -DBDL_NT_LOAD / -DBDL_NT_STORE (or -DBDL_NT for both; the default build).
-// Every vector is touched once per step and is far larger than the 256 MiB
-// Infinity Cache, so nothing is lost by not keeping lines resident.
-#ifdef BDL_NT
-#define BDL_NT_LOAD 1
-#define BDL_NT_STORE 1
-#endif
+// Every data-stream access is a non-temporal global access: each vector is
+// touched once per step and is far larger than the 256 MiB Infinity Cache.
+// The pointers are cast to the global address space explicitly: a gradient
+// base read from the LDS run table is a generic pointer to the compiler,
+// which would otherwise emit flat_load (counted on lgkmcnt as well as
+// vmcnt, so every LDS wait of the sweep also waited for it).
+typedef __attribute__((address_space(1))) f4v gf4v;
+typedef __attribute__((address_space(1))) float gfloat;
+
 __device__ __forceinline__ f4v vload(const float* p) {
-#ifdef BDL_NT_LOAD
-  return __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
-#else
-  return *reinterpret_cast<const f4v*>(p);
-#endif
+  return __builtin_nontemporal_load((const gf4v*)p);
 }
 
 __device__ __forceinline__ void vstore(float* p, f4v v) {
-#if defined(BDL_STORE_POLICY)
-  // A/B experiments: explicit cache-policy bits (1: sc1, 2: nt sc1, 3: sc0 sc1,
-  // 4: the compiler's nontemporal store = "nt")
-#if BDL_STORE_POLICY == 4
-  __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
-#elif BDL_STORE_POLICY == 5
-  // "nt sc1" through the raw-buffer builtin (hipcc tracks it: waitcnts and
-  // hazards handled by the compiler).  Wave-uniform base = the first active
-  // lane's address; every lane's 32-bit offset from it is >= 0 because the
-  // data-stream addresses increase with the lane id.
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  const uintptr_t base = ((uintptr_t)hi << 32) | lo;
-  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
-  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), rs, (int)(a - base), 0,
-                                         18 /* nt | sc1 */);
-#elif BDL_STORE_POLICY == 1
-  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
-#elif BDL_STORE_POLICY == 2
-  asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
-#else
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
-#endif
-#elif defined(BDL_NT_STORE)
-  // production: the compiler's non-temporal store ("nt").  Store-policy A/B
-  // (`make storepolicy P=<n>`, alternating full bench runs): "nt sc1"
-  // (write-through) read 1.3 % faster on a first box (asm form, before its
-  // store-data hazard was fixed with s_nop) and 0.6 % slower on a second box
-  // (hazard-free asm form and buffer-builtin form alike) — no consistent
-  // gain, so the compiler-tracked store stays.
-  __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
-#else
-  *reinterpret_cast<f4v*>(p) = v;
-#endif
+  __builtin_nontemporal_store(v, (gf4v*)p);
 }
+
+__device__ __forceinline__ float sload(const float* p) { return *(const gfloat*)p; }
+__device__ __forceinline__ void sstore(float* p, float v) { *(gfloat*)p = v; }
 
 __device__ __forceinline__ f4v ld4(const float* __restrict__ p, int64_t e, int64_t n) {
   if (e + 4 <= n) return vload(p + e);
   f4v v = {0.f, 0.f, 0.f, 0.f};
-  if (e + 0 < n) v.x = p[e + 0];
-  if (e + 1 < n) v.y = p[e + 1];
-  if (e + 2 < n) v.z = p[e + 2];
+  if (e + 0 < n) v.x = sload(p + e + 0);
+  if (e + 1 < n) v.y = sload(p + e + 1);
+  if (e + 2 < n) v.z = sload(p + e + 2);
   return v;
 }
 
@@ -173,9 +137,9 @@ __device__ __forceinline__ void st4(float* __restrict__ p, int64_t e, int64_t n,
     vstore(p + e, v);
     return;
   }
-  if (e + 0 < n) p[e + 0] = v.x;
-  if (e + 1 < n) p[e + 1] = v.y;
-  if (e + 2 < n) p[e + 2] = v.z;
+  if (e + 0 < n) sstore(p + e + 0, v.x);
+  if (e + 1 < n) sstore(p + e + 1, v.y);
+  if (e + 2 < n) sstore(p + e + 2, v.z);
 }
 
 struct KArgs {
@@ -204,12 +168,6 @@ struct KArgs {
   float* __restrict__ adam_v;
   float* __restrict__ sgd_buf;
   float b1, omb1, b2, omb2, bc1, bc2, aeps, two_alpha, nd, temp;
-  // Adam state tiling (bdl_adam_args.tile_log2 > 0): the streams of `tiled`
-  // (bit 0 mom, 1 adam_m, 2 adam_v, 3 sgd_buf) are interleaved in one
-  // allocation, 2^tshift float4 groups per stream per tile, tstride groups per
-  // tile of all streams; each pointer is its stream's base in tile 0
-  int32_t tshift, tiled;
-  int64_t tstride;
   // scalar-divisor reciprocals for BDL_FLAG_RECIP_DIV (host-rounded fl32(1/s64))
   float inv_s2, inv_nd, inv_ca, inv_cb, inv_temp, inv_bc1, inv_bc2;
 };
@@ -219,7 +177,21 @@ struct KArgs {
 // at [4*cgroups*k, 4*cgroups*(k+1))) chain k is keyed chain + k and draws what
 // a one-chain launch with that chain id draws.  The host keeps every group
 // index below 2^32 in that mode, so the split is a 32-bit division.
-__device__ __forceinline__ f4v step_noise4(const KArgs& a, int64_t gi) {
+__device__ __forceinline__ f4v step_noise4(const KArgs& a0, int64_t gi) {
+#ifdef BDL_PHILOX_KEYS_PER_CALL
+  // the generator's inputs (seed, chain, step, offset, chain split) re-read
+  // from the kernarg segment per call (scalar loads) instead of being held in
+  // SGPRs across the sweep (see philox4x32_10).  Every kernel that draws
+  // step noise takes its KArgs as the first kernel argument, at offset 0 of
+  // the segment.
+  (void)a0;
+  typedef __attribute__((address_space(4))) const KArgs ckargs;
+  ckargs* ap = (ckargs*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(ap));
+  ckargs& a = *ap;
+#else
+  const KArgs& a = a0;
+#endif
   uint64_t g = (uint64_t)gi + a.goff, c = a.chain;
   if (a.cgroups) {
     const uint32_t k = (uint32_t)g / a.cgroups;
@@ -426,22 +398,12 @@ __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, i
   constexpr bool kPriorLoad = T::kReadPrior && PRIOR && !GR;
   f4v th[UNROLL], g[UNROLL], v[UNROLL], t0[UNROLL], ep[UNROLL], m1[UNROLL], m2[UNROLL];
   const f4v z = {0.f, 0.f, 0.f, 0.f};
-#ifdef BDL_LOAD_STREAM_MAJOR
-  // A/B experiment (tools/step_ab.py): theta, grad, mom each issued for all
-  // unrolled groups before the next stream, instead of group by group
-#pragma unroll
-  for (int u = 0; u < UNROLL; ++u) th[u] = vload(a.theta + (gb + (int64_t)u * kBlock + threadIdx.x) * 4);
-#pragma unroll
-  for (int u = 0; u < UNROLL; ++u) g[u] = vload(gp + (gb + (int64_t)u * kBlock + threadIdx.x) * 4);
-#endif
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
     const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
     v[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
-#ifndef BDL_LOAD_STREAM_MAJOR
     th[u] = vload(a.theta + e);
     g[u] = vload(gp + e);
-#endif
     if constexpr (T::kMom) v[u] = vload(a.mom + e);
     if constexpr (METHOD == BDL_SGLD) {
       if (c.sgd_mom_read) v[u] = vload(a.mom + e);
@@ -577,10 +539,10 @@ __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, i
       while (rr < a.nruns - 1 && run_end(rr) <= e + j) ++rr;
       const uint32_t at = run_attr(rr);
       float* gpr = gt ? run_grad(a, rr) : nullptr;
-      if (gt && !gvec && !(at & BDL_ATTR_SKIP)) g[j] = gpr[e + j];
+      if (gt && !gvec && !(at & BDL_ATTR_SKIP)) g[j] = sload(gpr + e + j);
       float xt = th[j], xg = g[j], xv = v[j], x1 = m1[j], x2 = m2[j];
       update_elem<METHOD, NOISE, COLLECT, RECIP>(a, c, at, xt, xg, xv, t0[j], ep[j], x1, x2);
-      if (T::kWriteGrad && gt && !(at & BDL_ATTR_SKIP)) gpr[e + j] = xg;
+      if (T::kWriteGrad && gt && !(at & BDL_ATTR_SKIP)) sstore(gpr + e + j, xg);
       th[j] = xt;
       g[j] = xg;
       v[j] = xv;
@@ -601,6 +563,88 @@ __device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, i
   }
 }
 
+
+// Block-uniform test for the multi-run path: the full iteration whose
+// elements end at e_end starts in run r and ends in a later run; every run it
+// touches must allow the fast path (no SKIP, gradient base 16-B addressable)
+// and every run boundary inside it must fall on a float4 group boundary, so
+// that each lane's group lies in one run.
+__device__ __forceinline__ bool multi_run_ok(int nruns, int r, int64_t e_end) {
+  for (; r < nruns; ++r) {
+    if (run_attr(r) & kNoFastPath) return false;
+    const int64_t end = run_end(r);
+    if (end >= e_end) return true;
+    if (end & 3) return false;
+  }
+  return false;
+}
+
+// MULTI-RUN PATH: a whole block iteration in range that crosses run
+// boundaries (multi_run_ok).  Each lane finds the run of each of its groups
+// in the LDS table and applies that run's attributes (lr group, prior) per
+// element, reading the gradient from that run's own base; as on the fast
+// path every access is a 16-B access and every load is issued before any
+// arithmetic.  Where it is taken: iterations that straddle a tensor boundary
+// when each tensor's gradient is read from its own autograd allocation (one
+// run per tensor: ~300 of the ~75 K iterations of a ViT-L/32 step), which
+// the guarded slow path used to take with its loads serialised per group.
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
+__device__ __forceinline__ void chunk_multi(const KArgs& a, const StepConst& c, int64_t gb,
+                                            int r0, uint32_t& bad) {
+  using T = StepTraits<METHOD, COLLECT>;
+  f4v th[UNROLL], g[UNROLL], v[UNROLL], t0[UNROLL], ep[UNROLL], m1[UNROLL], m2[UNROLL];
+  uint32_t at[UNROLL];
+  float* gq[UNROLL];
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+  int rr = r0;  // a lane's groups only move forward; multi_run_ok bounds the search
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+    while (run_end(rr) <= e) ++rr;
+    at[u] = run_attr(rr);
+    gq[u] = run_grad(a, rr);
+    v[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
+    th[u] = vload(a.theta + e);
+    g[u] = vload(gq[u] + e);
+    if (T::kMom || (METHOD == BDL_SGLD && c.sgd_mom_read)) v[u] = vload(a.mom + e);
+    if (T::kReadPrior) t0[u] = vload(a.prior_mean + e);
+    if (NOISE == BDL_NOISE_BUFFER) ep[u] = vload(a.noise + e);
+    if (T::kReadMoments) {
+      m1[u] = vload(a.mom1 + e);
+      if (c.has_m2) m2[u] = vload(a.mom2 + e);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    const int64_t e = gi * 4;
+    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = step_noise4(a, gi);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float xt = th[u][j], xg = g[u][j], xv = v[u][j], x1 = m1[u][j], x2 = m2[u][j];
+      update_elem<METHOD, NOISE, COLLECT, RECIP>(a, c, at[u], xt, xg, xv, t0[u][j], ep[u][j], x1,
+                                                 x2);
+      th[u][j] = xt;
+      g[u][j] = xg;
+      v[u][j] = xv;
+      m1[u][j] = x1;
+      m2[u][j] = x2;
+    }
+    if constexpr (T::kWriteTheta) {
+      bad |= nonfinite4(th[u]);
+      vstore(a.theta + e, th[u]);
+    }
+    if constexpr (T::kWriteGrad) {
+      bad |= nonfinite4(g[u]);
+      vstore(gq[u] + e, g[u]);
+    }
+    if (T::kMom || (METHOD == BDL_SGLD && c.sgd_mom)) vstore(a.mom + e, v[u]);
+    if constexpr (T::kCollect) {
+      vstore(a.mom1 + e, m1[u]);
+      if (c.has_m2) vstore(a.mom2 + e, m2[u]);
+    }
+  }
+}
 
 template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
 __device__ __forceinline__ void step_body(const KArgs& a) {
@@ -644,10 +688,12 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
     while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
     const int64_t gend = min(gb + kIter, g1);
     const uint32_t attr = run_attr(r);
-    if (gend == gb + kIter && gend <= nfull && run_end(r) >= gend * 4 &&
-        !(attr & kNoFastPath))
+    const bool full = gend == gb + kIter && gend <= nfull;
+    if (full && run_end(r) >= gend * 4 && !(attr & kNoFastPath))
       chunk_fast_dispatch<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, attr, run_grad(a, r),
                                                                   bad);
+    else if (full && multi_run_ok(a.nruns, r, gend * 4))
+      chunk_multi<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, r, bad);
     else
       chunk_slow<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, gend, r, bad);
   }
@@ -712,25 +758,6 @@ __device__ __forceinline__ void adam_core(const KArgs& a, const AdamConst& c, fl
   }
 }
 
-// Element offset of float4 group gi in a tiled Adam state stream (e = 4 gi in
-// a separate vector).
-__device__ __forceinline__ int64_t tiled_elem(const KArgs& a, int64_t gi) {
-  const int64_t lo = gi & ((int64_t(1) << a.tshift) - 1);
-  return ((gi >> a.tshift) * a.tstride + lo) * 4;
-}
-
-// Offsets of group gi in (mom, adam_m, adam_v, sgd_buf): tiled or flat.
-struct AdamOff {
-  int64_t vm, m, v, b;
-};
-__device__ __forceinline__ AdamOff adam_offsets(const KArgs& a, int64_t gi) {
-  const int64_t e = gi * 4;
-  if (!a.tiled) return AdamOff{e, e, e, e};
-  const int64_t te = tiled_elem(a, gi);
-  return AdamOff{(a.tiled & 1) ? te : e, (a.tiled & 2) ? te : e, (a.tiled & 4) ? te : e,
-                 (a.tiled & 8) ? te : e};
-}
-
 template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, bool PRIOR, int U>
 __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, int64_t gb,
                                           float eta, float* gp, uint32_t& bad) {
@@ -741,14 +768,13 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
   for (int u = 0; u < U; ++u) {
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
     const int64_t e = gi * 4;
-    const AdamOff o = adam_offsets(a, gi);
     buf[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
     th[u] = vload(a.theta + e);
     g[u] = vload(gp + e);
-    vm[u] = vload(a.mom + o.vm);
-    m[u] = vload(a.adam_m + o.m);
-    v[u] = vload(a.adam_v + o.v);
-    if (!GRADONLY && c.sgd_mom_read) buf[u] = vload(a.sgd_buf + o.b);
+    vm[u] = vload(a.mom + e);
+    m[u] = vload(a.adam_m + e);
+    v[u] = vload(a.adam_v + e);
+    if (!GRADONLY && c.sgd_mom_read) buf[u] = vload(a.sgd_buf + e);
     if constexpr (PRIOR) t0[u] = vload(a.prior_mean + e);
     if constexpr (NOISE == BDL_NOISE_BUFFER) ep[u] = vload(a.noise + e);
     if constexpr (kReadMoments) {
@@ -780,7 +806,6 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
       m1[u][j] = x1;
       m2[u][j] = x2;
     }
-    const AdamOff o = adam_offsets(a, gi);
     if constexpr (GRADONLY) {
       bad |= nonfinite4(g[u]);
       vstore(gp + e, g[u]);
@@ -788,10 +813,10 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
       bad |= nonfinite4(th[u]);
       vstore(a.theta + e, th[u]);
     }
-    vstore(a.mom + o.vm, vm[u]);
-    vstore(a.adam_m + o.m, m[u]);
-    vstore(a.adam_v + o.v, v[u]);
-    if (!GRADONLY && c.sgd_mom) vstore(a.sgd_buf + o.b, buf[u]);
+    vstore(a.mom + e, vm[u]);
+    vstore(a.adam_m + e, m[u]);
+    vstore(a.adam_v + e, v[u]);
+    if (!GRADONLY && c.sgd_mom) vstore(a.sgd_buf + e, buf[u]);
     if constexpr (COLLECT != BDL_COLLECT_NONE) {
       vstore(a.mom1 + e, m1[u]);
       if (c.has_m2) vstore(a.mom2 + e, m2[u]);
@@ -813,14 +838,7 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
     if (gi >= gend) continue;
     const int64_t e = gi * 4;
     const bool gt = a.gbase != nullptr;  // gradient per tensor (as in chunk_slow)
-    // tiled streams: the pointer shifted so that index e lands on the group's
-    // tiled slot (ld4 / st4 keep their bound on the flat index)
-    const AdamOff o = adam_offsets(a, gi);
-    float* const pvm = a.mom + (o.vm - e);
-    float* const pm = a.adam_m + (o.m - e);
-    float* const pv = a.adam_v + (o.v - e);
-    float* const pb = a.sgd_buf ? a.sgd_buf + (o.b - e) : nullptr;
-    f4v th = ld4(a.theta, e, n), g = gt ? z : ld4(a.grad, e, n), vm = ld4(pvm, e, n);
+    f4v th = ld4(a.theta, e, n), g = gt ? z : ld4(a.grad, e, n), vm = ld4(a.mom, e, n);
     bool gvec = false;
     if (gt) {
       while (rr < a.nruns - 1 && run_end(rr) <= e) ++rr;
@@ -829,9 +847,9 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
         gvec = true;
       }
     }
-    f4v m = ld4(pm, e, n), v = ld4(pv, e, n), t0 = ld4(a.prior_mean, e, n);
+    f4v m = ld4(a.adam_m, e, n), v = ld4(a.adam_v, e, n), t0 = ld4(a.prior_mean, e, n);
     f4v buf = z, ep = z, m1 = z, m2 = z;
-    if (!GRADONLY && c.sgd_mom_read) buf = ld4(pb, e, n);
+    if (!GRADONLY && c.sgd_mom_read) buf = ld4(a.sgd_buf, e, n);
     if (NOISE == BDL_NOISE_BUFFER) ep = ld4(a.noise, e, n);
     if (NOISE == BDL_NOISE_PHILOX) ep = step_noise4(a, gi);
     if (COLLECT == BDL_COLLECT_MEAN) {
@@ -843,7 +861,7 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
       while (rr < a.nruns - 1 && run_end(rr) <= e + j) ++rr;
       const uint32_t at = run_attr(rr);
       float* gpr = gt ? run_grad(a, rr) : nullptr;
-      if (gt && !gvec && !(at & BDL_ATTR_SKIP)) g[j] = gpr[e + j];
+      if (gt && !gvec && !(at & BDL_ATTR_SKIP)) g[j] = sload(gpr + e + j);
       float xt = th[j], xg = g[j], xvm = vm[j], xm = m[j], xv = v[j], xb = buf[j];
       float x1 = m1[j], x2 = m2[j];
       if (!(at & BDL_ATTR_SKIP)) {
@@ -854,7 +872,7 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
           adam_core<NOISE, RECIP, false, GRADONLY>(a, c, eta, xt, xg, xvm, xm, xv, xb, t0[j], ep[j]);
       }
       collect_core<COLLECT, RECIP>(a, cc, xt, x1, x2);
-      if (GRADONLY && gt && !(at & BDL_ATTR_SKIP)) gpr[e + j] = xg;
+      if (GRADONLY && gt && !(at & BDL_ATTR_SKIP)) sstore(gpr + e + j, xg);
       th[j] = xt;
       g[j] = xg;
       vm[j] = xvm;
@@ -871,10 +889,10 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
       bad |= nonfinite4(th);
       st4(a.theta, e, n, th);
     }
-    st4(pvm, e, n, vm);
-    st4(pm, e, n, m);
-    st4(pv, e, n, v);
-    if (!GRADONLY && c.sgd_mom) st4(pb, e, n, buf);
+    st4(a.mom, e, n, vm);
+    st4(a.adam_m, e, n, m);
+    st4(a.adam_v, e, n, v);
+    if (!GRADONLY && c.sgd_mom) st4(a.sgd_buf, e, n, buf);
     if (COLLECT != BDL_COLLECT_NONE) {
       st4(a.mom1, e, n, m1);
       if (c.has_m2) st4(a.mom2, e, n, m2);
@@ -884,8 +902,7 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
 
 
 // ---------------------------------------------------------------------------
-// Software-pipelined Adam sweep (not GRADONLY; the production path unless
-// built with -DBDL_ADAM_NO_PIPE): the next block iteration's loads are issued
+// Software-pipelined Adam sweep (not GRADONLY): the next block iteration's loads are issued
 // before this iteration's arithmetic, so the ~420 VALU instructions per float4
 // group (IEEE divide / sqrt x2 each, Philox) run while the next seven streams
 // are in flight.  One process, same buffers, alternating builds
@@ -910,13 +927,12 @@ __device__ __forceinline__ void adam_pipe_load(const KArgs& a, const AdamConst& 
   for (int u = 0; u < U; ++u) {
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
     const int64_t e = gi * 4;
-    const AdamOff o = adam_offsets(a, gi);
     R.th[u] = vload(a.theta + e);
     R.g[u] = vload(gp + e);
-    R.vm[u] = vload(a.mom + o.vm);
-    R.m[u] = vload(a.adam_m + o.m);
-    R.v[u] = vload(a.adam_v + o.v);
-    R.buf[u] = c.sgd_mom_read ? vload(a.sgd_buf + o.b) : z;
+    R.vm[u] = vload(a.mom + e);
+    R.m[u] = vload(a.adam_m + e);
+    R.v[u] = vload(a.adam_v + e);
+    R.buf[u] = c.sgd_mom_read ? vload(a.sgd_buf + e) : z;
     R.t0[u] = prior ? vload(a.prior_mean + e) : z;
     R.ep[u] = z;
     if constexpr (NOISE == BDL_NOISE_BUFFER) R.ep[u] = vload(a.noise + e);
@@ -956,13 +972,12 @@ __device__ __forceinline__ void adam_pipe_compute(const KArgs& a, const AdamCons
       R.m1[u][j] = x1;
       R.m2[u][j] = x2;
     }
-    const AdamOff o = adam_offsets(a, gi);
     bad |= nonfinite4(R.th[u]);
     vstore(a.theta + e, R.th[u]);
-    vstore(a.mom + o.vm, R.vm[u]);
-    vstore(a.adam_m + o.m, R.m[u]);
-    vstore(a.adam_v + o.v, R.v[u]);
-    if (c.sgd_mom) vstore(a.sgd_buf + o.b, R.buf[u]);
+    vstore(a.mom + e, R.vm[u]);
+    vstore(a.adam_m + e, R.m[u]);
+    vstore(a.adam_v + e, R.v[u]);
+    if (c.sgd_mom) vstore(a.sgd_buf + e, R.buf[u]);
     if constexpr (COLLECT != BDL_COLLECT_NONE) {
       vstore(a.mom1 + e, R.m1[u]);
       if (c.has_m2) vstore(a.mom2 + e, R.m2[u]);
@@ -1065,14 +1080,12 @@ __device__ __forceinline__ void adam_body(const KArgs& a) {
   constexpr int64_t kIter = (int64_t)kBlock * U;
   const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
   stage_runs(a);
-#ifndef BDL_ADAM_NO_PIPE
-  if constexpr (!GRADONLY) {  // production: the software-pipelined sweep
+  if constexpr (!GRADONLY) {  // the software-pipelined sweep
     uint32_t bad = 0;
     adam_pipe_sweep<NOISE, COLLECT, RECIP, U>(a, c, bad);
     report_nonfinite(a, bad);
     return;
   }
-#endif
   int r = find_run_lds(a.nruns, (int64_t)blockIdx.x * kIter * 4);
   uint32_t bad = 0;
   for (int64_t gb = (int64_t)blockIdx.x * kIter; gb < ngroups; gb += (int64_t)gridDim.x * kIter) {
@@ -1107,12 +1120,6 @@ __global__ __launch_bounds__(kBlock) void bdl_adam_kernel(const KArgs a) {
 // ---------------------------------------------------------------------------
 using StepKernel = void (*)(const KArgs);
 
-// A/B flavours only (make flavor D=-DBDL_DEEP_UNROLL=8): the depth that an
-// unroll-4 request runs at
-#ifndef BDL_DEEP_UNROLL
-#define BDL_DEEP_UNROLL 4
-#endif
-
 template <int METHOD, int NOISE, int COLLECT>
 StepKernel pick_unroll(int unroll) {
   // Every unroll depth for cSGHMC and for the noise-bearing SGHMC / SGLD
@@ -1129,7 +1136,7 @@ StepKernel pick_unroll(int unroll) {
       case 1:
         return bdl_step_kernel<METHOD, NOISE, COLLECT, 1>;
       case 4:
-        return bdl_step_kernel<METHOD, NOISE, COLLECT, BDL_DEEP_UNROLL>;
+        return bdl_step_kernel<METHOD, NOISE, COLLECT, 4>;
       default:
         return bdl_step_kernel<METHOD, NOISE, COLLECT, 2>;
     }

@@ -70,142 +70,6 @@ def build_runs(offsets, numels, attrs, n):
     return out
 
 
-PLACEMENT_MIN_ELEMS = 1 << 24  # below ~64 MB per vector placement effects are noise
-
-
-def _placement_launcher(method, vs, n, device, runs):
-    """The sampler's update on scratch vectors `vs` (role -> tensor), launched
-    as the placement probe (BDL_FLAG_PLACEMENT_PROBE: the production update
-    under its own kernel symbol, so placement timing never mixes into a
-    kernel-trace summary of the production kernels).  cSGHMC: the explore
-    update (theta rw, grad r, mom rw); SGLD and the Adam variants: SGLD + SGD
-    momentum with Philox noise (theta rw, grad r, prior r, buffer rw — the
-    theta / buffer pairing placement optimises)."""
-    from types import SimpleNamespace
-
-    from . import kernels as K
-    st = SimpleNamespace(theta=vs["theta"], grad=vs["grad"], mom=vs.get("mom"),
-                         prior=vs.get("prior"), noise=None, runs=runs, nruns=1, n=n,
-                         device=device)
-    if method == "csghmc":
-        return lambda: K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-4, 1e-4), noise_scale=(0.0, 0.0),
-                                     noise_mode=L.NOISE_NONE, one_minus_alpha=0.9, prior_sig=1.0,
-                                     probe=True)
-    if method in ("sgld", "adam"):
-        return lambda: K.sgmcmc_step(st, L.SGLD, lrs=(1e-4, 1e-4), noise_scale=(1e-3, 1e-3),
-                                     noise_mode=L.NOISE_PHILOX, sigma2=1.0, n_data=1e6, mu=0.5,
-                                     momentum=st.mom is not None, probe=True)
-    raise ValueError(f"placed_vectors: unknown method {method!r}")
-
-
-def _time_launch(launch, device, reps=5):
-    launch()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(reps)]
-    for e0, e1 in ev:
-        e0.record()
-        launch()
-        e1.record()
-    torch.cuda.synchronize(device)
-    return float(np.median([a.elapsed_time(b) for a, b in ev]))
-
-
-PLACEMENT_BPC = {"csghmc": 1, "sgld": 2, "adam": 2}  # workgroups/CU of the placement probe
-
-
-def placed_vectors(n, device, names, method, park=False):
-    """Allocate the chain's swept fp32 vectors (`names` among theta, grad, mom,
-    prior, extra state), zeroed.  With `method` (the sampler's kernel family)
-    and vectors of >= PLACEMENT_MIN_ELEMS, the read-modify-write vectors are
-    built from physical chunks with theta and mom paired fast
-    (bayesdll_amd.placement's bounded search; DESIGN.md §4 "Placement"); a
-    gradient vector is always a plain torch allocation, like the gradients
-    autograd hands the Runners.  Otherwise, or when the driver refuses chunk
-    mappings, torch's allocator.  BDL_PLACEMENT: "0" (torch's allocator, the
-    default), "search", "order" (chunks in allocation order, no timing).
-    park: the placed set is parked when its vectors die (the autotuner's
-    scratch state, whose set the chain state then takes).
-    Returns ({name: tensor}, info or None)."""
-    from . import placement as P
-    f32 = dict(dtype=torch.float32, device=device)
-    mode = P.mode()
-    if method is None or n < PLACEMENT_MIN_ELEMS or "mom" not in names or "theta" not in names \
-            or mode == "0":
-        return {nm: torch.zeros(n, **f32) for nm in names}, None
-    free, _ = torch.cuda.mem_get_info(device)
-    runs_by_n = {}
-    pnames = [nm for nm in names if nm != "grad"]
-    grad = torch.zeros(n, **f32) if "grad" in names else None
-    per, cb = P.chunk_geometry(n)
-    gsrc = grad if grad is not None and cb // 4 <= n else torch.zeros(max(n, cb // 4), **f32)
-
-    def launcher(roles, m):
-        if m not in runs_by_n:
-            runs_by_n[m] = build_runs([0], [m], [L.ATTR_PRIOR], m).to(device)
-        return _placement_launcher(method, {"grad": gsrc[:m], **roles}, m, device, runs_by_n[m])
-
-    from . import kernels as K
-    # the probe kernel's depth is fixed at 4; workgroups per CU: the method's
-    # usual optimum at that depth (cSGHMC 1, the VALU-heavier SGLD / Adam
-    # sweeps 2 — at 1 they are occupancy-bound and placement barely shows),
-    # whatever geometry another state installed
-    prev = K.set_launch_config(PLACEMENT_BPC.get(method, 1), 4, 1)
-    try:
-        vecs, info = P.place(n, device, pnames, launcher, lambda f: _time_launch(f, device, 5),
-                             budget_bytes=int(0.25 * free), search=mode == "search",
-                             pool_key=(method,), park=park)
-    except RuntimeError as e:  # chunk mappings unavailable / over budget: plain allocations
-        import warnings
-        warnings.warn(f"bayesdll_amd: physical-chunk placement unavailable ({e}); "
-                      "using torch's allocator")
-        return {nm: torch.zeros(n, **f32) for nm in names}, {"allocator": "torch",
-                                                             "error": str(e)[:200]}
-    finally:
-        K.restore_launch_config(prev)
-        del gsrc
-    info = dict(info, method=method)
-    if grad is not None:
-        vecs["grad"] = grad
-    return vecs, info
-
-
-def placed_moments(theta, need_m2=True):
-    """(m1, m2) running-moment vectors of theta's size for the stand-alone
-    bdl_moments_update sweep (methods/sgld.py:95-102 seeding, :236-246 the
-    running mean; theta r, m1 rw, m2 rw), zeroed, placed the way the step's
-    theta / mom pair is: that sweep is fast iff its two read-modify-write
-    streams m1 / m2 sit in different physical groups, so the
-    pair goes through the same bounded search with the moments kernel as the
-    timed launch (roles theta -> m1, mom -> m2).  Below PLACEMENT_MIN_ELEMS,
-    without m2, or with BDL_PLACEMENT=0: plain allocations.  Values never
-    depend on it.  Returns (m1, m2, info)."""
-    from . import placement as P
-    n, device = theta.numel(), theta.device
-    mode = P.mode()
-    if not need_m2 or n < PLACEMENT_MIN_ELEMS or mode == "0":
-        return (torch.zeros_like(theta), torch.zeros_like(theta) if need_m2 else None, None)
-    from . import kernels as K
-
-    def launcher(roles, m):
-        k = min(m, n)  # a one-chunk vector's chunk is rounded up past n
-        src, m1, m2 = theta[:k], roles["theta"][:k], roles["mom"][:k]
-        return lambda: K.moments_update(src, m1, m2, L.COLLECT_MEAN, collect_a=3.0,
-                                        collect_b=4.0)
-
-    free, _ = torch.cuda.mem_get_info(device)
-    try:
-        vecs, info = P.place(n, device, ["theta", "mom"], launcher,
-                             lambda f: _time_launch(f, device, 5), budget_bytes=int(0.25 * free),
-                             search=mode == "search", pool_key=("moments",))
-    except RuntimeError as e:  # chunk mappings unavailable: plain allocations
-        import warnings
-        warnings.warn(f"bayesdll_amd: physical-chunk placement unavailable ({e}); "
-                      "using torch's allocator")
-        return torch.zeros_like(theta), torch.zeros_like(theta), {"allocator": "torch",
-                                                                  "error": str(e)[:200]}
-    return vecs["theta"], vecs["mom"], dict(info, method="moments")
-
-
 GRAD_MODES = ("tensor", "flat")
 MAX_TENSOR_RUNS = 2730  # 24 B per run in 64 KiB of LDS (bdl_step_args.grad_base)
 GRAD_TABLE_CACHE = 8  # device run/base tables kept per state (one per pointer set)
@@ -224,8 +88,7 @@ class FlatState:
     gradient mode, grads)."""
 
     def __init__(self, net, net0=None, *, readout_name=None, bias="informative",
-                 need_prior=False, need_mom=True, need_noise=False, placement=None,
-                 extra=(), grad_mode=None):
+                 need_prior=False, need_mom=True, need_noise=False, extra=(), grad_mode=None):
         named = list(net.named_parameters())
         if not named:
             raise ValueError("bayesdll_amd: the network has no parameters")
@@ -255,17 +118,14 @@ class FlatState:
                           f"{MAX_TENSOR_RUNS}: using the flat gradient vector")
             self.grad_mode = "flat"
 
-        # the swept vectors, placed (see placed_vectors) when `placement` names
-        # the sampler's kernel family (in "tensor" mode the timing uses a
-        # scratch gradient vector, freed after the choice)
-        names_ = ["theta", "grad"] + (["mom"] if need_mom else []) + \
-            (["prior"] if need_prior else []) + list(extra)
-        vecs, self.placement_info = placed_vectors(self.n, dev, names_, placement)
-        if self.grad_mode == "tensor":
-            del vecs["grad"]
+        # the swept vectors, each one allocation from torch's caching allocator
+        # (no flat gradient vector in "tensor" mode)
+        names_ = ["theta"] + (["grad"] if self.grad_mode == "flat" else []) + \
+            (["mom"] if need_mom else []) + (["prior"] if need_prior else []) + list(extra)
+        vecs = {nm: torch.zeros(self.n, dtype=torch.float32, device=dev) for nm in names_}
         # further per-element state of the sampler (e.g. Adam's m, v and the
-        # SGD buffer), placed together with the swept vectors, zeroed
-        self.extra = {nm: vecs[nm].zero_() for nm in extra}
+        # SGD buffer), zeroed
+        self.extra = {nm: vecs[nm] for nm in extra}
         # theta: copy then rebind every parameter as a view (same storage order
         # as nn.utils.parameters_to_vector)
         self.theta = vecs["theta"]
@@ -319,11 +179,9 @@ class FlatState:
 
     @classmethod
     def from_segments(cls, segments, readout_name, *, bias="informative", device="cuda",
-                      need_prior=False, need_mom=True, need_noise=False, init=None,
-                      placement=None, extra=(), park=False):
+                      need_prior=False, need_mom=True, need_noise=False, init=None, extra=()):
         """Flat chain state for a segment table alone (no nn.Module): the
-        benchmark and kernel tests use it with synthetic vectors.  park: its
-        placed set is parked when it dies (placement.PlacedSet)."""
+        benchmark and kernel tests use it with synthetic vectors."""
         self = cls.__new__(cls)
         self.names = [nm for nm, _ in segments]
         self.shapes = [tuple(s) for _, s in segments]
@@ -341,9 +199,8 @@ class FlatState:
         f32 = dict(dtype=torch.float32, device=self.device)
         names_ = (["theta"] if init is None else []) + ["grad"] + (["mom"] if need_mom else []) \
             + (["prior"] if need_prior else []) + list(extra)
-        vecs, self.placement_info = placed_vectors(
-            self.n, self.device, names_, placement if init is None else None, park=park)
-        self.extra = {nm: vecs[nm].zero_() for nm in extra}
+        vecs = {nm: torch.zeros(self.n, **f32) for nm in names_}
+        self.extra = {nm: vecs[nm] for nm in extra}
         self.theta = vecs["theta"] if init is None else init
         self.grad_mode = "flat"
         self.gbase = None
@@ -628,45 +485,23 @@ def bind_parameters(net, flat=None):
     return flat
 
 
-DRAW_CANDIDATES = 3  # output buffers timed for the posterior-draw sweep
-
-
-def draw_buffer(out, launch, candidates=DRAW_CANDIDATES):
-    """Pick the posterior-draw output buffer: the draw reads m1 / m2 and
-    writes out, and its speed depends on out's physical memory relative to
-    its reads, which only timing reveals.  `launch(buf)` runs
-    the draw into `buf`; `out` and candidates - 1 fresh torch allocations of
-    its size are each timed (median of 3 launches) and the fastest returned
-    with {"torch_ms": [...], "kept": index}; the losers go back to torch's
-    cache.  Vectors below PLACEMENT_MIN_ELEMS, or BDL_PLACEMENT=0: (`out`,
-    None)."""
-    from . import placement as P
-    if out.numel() < PLACEMENT_MIN_ELEMS or P.mode() == "0":
-        return out, None
-    cands = [out] + [torch.empty_like(out) for _ in range(max(0, candidates - 1))]
-    ms = [_time_launch(lambda b=b: launch(b), out.device, 3) for b in cands]
-    best = int(np.argmin(ms))
-    return cands[best], {"torch_ms": [round(t, 4) for t in ms], "kept": best}
-
-
 MOMENT_PAIR_ALIGN = 64  # elements: m2 starts 256 B after a 256-B boundary
+MOMENT_PAIR_MIN_ELEMS = 1 << 24  # smaller pairs: two plain allocations
 
 
 def moment_pair(n, device):
     """(m1, m2) for one cycle's Welford / running moments (methods/csghmc.py:333-337,
     methods/csgld.py:282-293): the two halves of ONE allocation, m2 starting
-    on a 256-B boundary.  Why (DESIGN.md §4 placement): the posterior draw
-    (m1 r, m2 r, out w) runs 0.608-0.616 ms for ViT-L/32 with m1 / m2 in one
-    physical class and out in the other, 0.631-0.650 with m1 / m2 split
+    on a 256-B boundary.  Why: the posterior draw (m1 r, m2 r, out w) ran
+    0.608-0.616 ms for ViT-L/32 with m1 / m2 in one allocation against
+    0.631-0.650 with the two split over separately allocated physical memory
     (profiles/round2/placement/aux_roles/collect_and_sample_by_class.jsonl);
-    one allocation puts both halves in one class, and flat.draw_buffer then
-    picks an output buffer from the other.  The collect steps that fill them
-    do not care (1.754-1.762 ms over all four class combinations).  A layout,
-    not a search: taken whatever BDL_PLACEMENT says.  Vectors below
-    PLACEMENT_MIN_ELEMS: two plain allocations.  Values never depend on it;
-    torch.save of both halves in one call stores the shared storage once."""
+    the collect steps that fill them do not care (1.754-1.762 ms).  A layout,
+    not a search.  Pairs below MOMENT_PAIR_MIN_ELEMS: two plain allocations.
+    Values never depend on it; torch.save of both halves in one call stores
+    the shared storage once."""
     f32 = dict(dtype=torch.float32, device=device)
-    if n < PLACEMENT_MIN_ELEMS:
+    if n < MOMENT_PAIR_MIN_ELEMS:
         return torch.empty(n, **f32), torch.empty(n, **f32)
     stride = -(-n // MOMENT_PAIR_ALIGN) * MOMENT_PAIR_ALIGN
     buf = torch.empty(stride + n, **f32)
@@ -681,65 +516,3 @@ def fill_normal_per_tensor(vec, numels, generator=None):
         vec[off:off + k].normal_(generator=generator)
         off += k
     return vec
-
-
-TILE_LOG2_MAX = 20  # 2^20 float4 groups = 16 MiB per stream per tile
-
-
-class TiledState:
-    """Per-element sampler state streams (Adam's m, v, SGD buffer, ...)
-    interleaved in ONE allocation: tiles of 2^log2 float4 groups per stream,
-    `len(names)` streams per tile (bdl_adam_args.tile_*, include/bdl_sgmcmc.h).
-    Why: the Adam-SGHMC sweep reads seven and writes five
-    vectors; with the four state vectors as separate allocations its HBM rate
-    depends on where the allocator put them (2.42-2.76 ms for ViT-L/32 over
-    fresh allocations), as one region it does not (2.39-2.40 ms;
-    profiles/round4/layout_big/adam.jsonl, tools/layout_probe.hip).  Values never
-    depend on the layout.
-
-    `stream(name)` is the stream as a torch view: 1-D of n elements when the
-    vector fits one tile, else 2-D [tiles, tile elements] (the last tile's tail
-    past n is padding); `flat(name)` an n-element vector (a copy when 2-D);
-    `load(name, vec)` writes one."""
-
-    def __init__(self, n, names, device, log2=None):
-        self.n, self.names = int(n), tuple(names)
-        groups = max(1, -(-self.n // 4))
-        if log2 is None:
-            log2 = min(TILE_LOG2_MAX, max(0, (groups - 1).bit_length()))
-        self.log2 = max(1, int(log2))  # tile_log2 = 0 means "separate vectors" in the ABI
-        self.tile = 4 << self.log2      # elements per stream per tile
-        self.ntiles = -(-self.n // self.tile)
-        self.block = torch.zeros(self.ntiles * len(self.names) * self.tile, dtype=torch.float32,
-                                 device=device)
-        self._views = {}
-        for s, nm in enumerate(self.names):
-            v = torch.as_strided(self.block, (self.ntiles, self.tile),
-                                 (len(self.names) * self.tile, 1), s * self.tile)
-            self._views[nm] = v[0, :self.n] if self.ntiles == 1 else v
-
-    def stream(self, name):
-        return self._views[name]
-
-    def flat(self, name):
-        v = self._views[name]
-        return v if v.dim() == 1 else v.reshape(-1)[:self.n]
-
-    def load(self, name, vec):
-        v = self._views[name]
-        vec = vec.reshape(-1).to(device=v.device, dtype=torch.float32)
-        if v.dim() == 1:
-            v.copy_(vec)
-        else:
-            full = torch.zeros(self.ntiles * self.tile, dtype=torch.float32, device=v.device)
-            full[:self.n] = vec
-            v.copy_(full.view(self.ntiles, self.tile))
-
-    def abi(self, names):
-        """(tile_log2, tile_streams, tile_mask) for bdl_adam_args: `names` are
-        the kernel's stream slots in mask-bit order (mom, adam_m, adam_v, sgd_buf)."""
-        mask = 0
-        for bit, nm in enumerate(names):
-            if nm in self._views:
-                mask |= 1 << bit
-        return self.log2, len(self.names), mask

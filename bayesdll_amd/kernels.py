@@ -39,7 +39,7 @@ def _step_args(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1
                prior_sig=0.0, sigma2=1.0, n_data=1.0, mu=0.0, first_step=False,
                momentum=False, collect=L.COLLECT_NONE, mom1=None, mom2=None, collect_a=1.0,
                collect_b=1.0, seed=0, chain=0, step=0, div_mode=None, noise=None, grad_ready=False,
-               mom_buf=None, philox_offset=0, probe=False):
+               mom_buf=None, philox_offset=0):
     a = L.StepArgs()
     a.theta = state.theta.data_ptr()
     g = getattr(state, "grad", None)
@@ -61,8 +61,7 @@ def _step_args(state, method, *, lrs, noise_scale, noise_mode, one_minus_alpha=1
     a.noise_mode = int(noise_mode)
     a.collect = int(collect)
     a.flags = ((L.FLAG_FIRST_STEP if first_step else 0) | (L.FLAG_MOMENTUM if momentum else 0)
-               | (L.FLAG_GRAD_READY if grad_ready else 0) | _div_flag(div_mode)
-               | (L.FLAG_PLACEMENT_PROBE if probe else 0))
+               | (L.FLAG_GRAD_READY if grad_ready else 0) | _div_flag(div_mode))
     a.n = state.n
     a.lr[0], a.lr[1] = float(lrs[0]), float(lrs[1])
     a.noise_scale[0], a.noise_scale[1] = float(noise_scale[0]), float(noise_scale[1])
@@ -151,8 +150,11 @@ def _launch(state, fn, a, adam=None, written=None):
     # step's: 1.42 ms there vs 1.48 at the Welford collect's 1 x 1
     collect = a.collect in (L.COLLECT_WELFORD, L.COLLECT_MEAN)
     pend = getattr(state, "_tune_pending", None)
+    # a first step (SGD buffer written, not read) is not the steady-state
+    # access mix: the kind stays pending until a later launch
     if pend and written is not None and int(a.n) == int(state.n) and \
             ("collect" if collect else "step") in pend and \
+            not (a.flags & L.FLAG_FIRST_STEP) and \
             not torch.cuda.is_current_stream_capturing():
         _tune_kind(state, fn, collect, written)
     _use_geometry(state, collect)
@@ -193,13 +195,11 @@ def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps,
               momentum_decay, nd, temperature=1.0, grad_is_mom=False, lrs, noise_mode,
               sigma2, n_data, mu=0.0, first_step=False, momentum=False, collect=L.COLLECT_NONE,
               mom1=None, mom2=None, collect_a=1.0, collect_b=1.0, seed=0, chain=0, step=0,
-              div_mode=None, noise=None, philox_offset=0, tile=None):
+              div_mode=None, noise=None, philox_offset=0):
     """One fused Adam-preconditioned SGHMC step (methods/adam_sghmc.py:500-553,
     adam_csghmc.py:812-860) + SGD step.  The host-side scalars are formed in
     float64 exactly as the reference's Python does (1 - beta1, 1 - beta1**t,
-    2 * momentum_decay, 1 - momentum_decay); ctypes rounds them to fp32.
-    tile: (log2 float4 groups per tile, streams per tile, stream mask) when
-    the state streams live in a TiledState (bdl_adam_args.tile_*), else None."""
+    2 * momentum_decay, 1 - momentum_decay); ctypes rounds them to fp32."""
     a = _step_args(state, method, lrs=lrs, noise_scale=(0.0, 0.0), noise_mode=noise_mode,
                    one_minus_alpha=1 - momentum_decay, sigma2=sigma2, n_data=n_data, mu=mu,
                    first_step=first_step, momentum=momentum, collect=collect, mom1=mom1,
@@ -220,8 +220,6 @@ def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps,
     ad.inv_bias_corr1, ad.inv_bias_corr2 = _inv(bc1), _inv(bc2)
     ad.inv_temperature = _inv(temperature)
     ad.grad_is_mom = 1 if grad_is_mom else 0
-    if tile is not None:
-        ad.tile_log2, ad.tile_streams, ad.tile_mask = (int(x) for x in tile)
     wr = _written(state, method, grad_only=method == L.ADAM_SGHMC_GRAD, mom=state.mom,
                   extra=(adam_m, adam_v) + ((sgd_buf,) if sgd_buf is not None else ()),
                   mom1=mom1 if collect != L.COLLECT_NONE else None,
@@ -232,7 +230,7 @@ def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps,
 
 def stream_mix(reads, writes, blocks_per_cu=1, unroll=4):
     """The bare access mix of a sweep over these buffers (bdl_stream_mix,
-    include/bdl_placement.h): measurement only — the written tensors' contents
+    include/bdl_measure.h): measurement only — the written tensors' contents
     are destroyed.  Asynchronous, on the current stream."""
     n = reads[0].numel()
     dev = reads[0].device
@@ -305,15 +303,16 @@ def _tune_sample(a, out):
     0.635-0.653 for the best of the others on three boxes
     (profiles/round4/philox_ab/)."""
     stream = L.current_stream_handle(out.device)
+    ts = torch.cuda.current_stream(out.device)  # the stream the draws are launched on
     best = None
     for bpc, u in SAMPLE_GEOMETRIES:
         a.blocks_per_cu, a.unroll = bpc, u
         L.check(L.lib().bdl_posterior_sample(a, stream), "bdl_posterior_sample")
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        ev[0].record()
+        ev[0].record(ts)
         for _ in range(3):
             L.check(L.lib().bdl_posterior_sample(a, stream), "bdl_posterior_sample")
-        ev[1].record()
+        ev[1].record(ts)
         ev[1].synchronize()
         ms = ev[0].elapsed_time(ev[1])
         if best is None or ms < best[0]:
@@ -395,7 +394,7 @@ def _use_geometry(state, collect=False):
 # depths 1, 2 and 4.
 AUTOTUNE_CANDIDATES = ((2, 1, 1), (1, 4, 1), (3, 1, 1), (2, 4, 1), (1, 2, 1), (2, 2, 1))
 # per sampler family, the geometries that won somewhere in the interleaved
-# 13-geometry probe on a placed ViT-L/32 state (tools/geom_methods.py,
+# 13-geometry probe on a ViT-L/32 state (tools/geom_methods.py,
 # profiles/round3/aux/geom_methods.jsonl): SGLD 3 x 4 by 0.5 % over 2 x 4;
 # Adam-SGHMC 1 x 1 by 1.5 % and 4 x 4 by 0.3 % over 2 x 4 (seven streams: fewer
 # accesses in flight per CU pay); cSGHMC 1 x 4 by >= 1.9 % over every other
@@ -421,32 +420,22 @@ COLLECT_EXTRA = ((1, 1, 1),)
 ADAM_EXTRA = ("adam_m", "adam_v", "sgd_buf")  # adam_sghmc.Model.extra_vectors
 
 
-def _scratch_launcher(n, dev, method, placed=True):
+def _scratch_launcher(n, dev, method):
     """A closure launching `method`'s production kernel over scratch buffers of
     n elements (the buffers live as long as the closure)."""
-    return _scratch_launchers(n, dev, method, placed)[0]
+    return _scratch_launchers(n, dev, method)[0]
 
 
-def _scratch_launchers(n, dev, method, placed=True):
+def _scratch_launchers(n, dev, method):
     """Closures launching `method`'s production kernel over scratch buffers of
     n elements — (plain step, collect step: the same with the posterior-moment
     update; its m1 / m2 are allocated at its first call, for cSGHMC as the
     Runner allocates a cycle's Welford pair) — the buffers live as long as the
-    closures.  Large scratch vectors are placed like a chain's own
-    (flat.placed_vectors): on plain allocations that happen to pair slowly,
-    geometries rank differently than on the placed vectors the sampler then
-    sweeps (3 of 38 round-2 bench runs kept a geometry 1.5-3 % slower there
-    than 1 x 4)."""
-    from .flat import PLACEMENT_MIN_ELEMS, FlatState, moment_pair
-    # the same roles as the sampler's own state, so that its placed set, parked
-    # when this scratch state dies, is the one the sampler's state then takes
-    # (bayesdll_amd.placement pool: one search per process and size)
+    closures."""
+    from .flat import FlatState, moment_pair
     st = FlatState.from_segments([("w", (int(n),))], None, device=dev,
                                  need_prior=method != "csghmc",
-                                 placement=method if placed and int(n) >= PLACEMENT_MIN_ELEMS
-                                 else None,
-                                 extra=ADAM_EXTRA if method == "adam" else (),
-                                 park=True)
+                                 extra=ADAM_EXTRA if method == "adam" else ())
     st.theta.zero_()
     if method == "csghmc":
         kw = dict(lrs=(1e-4, 1e-4), noise_scale=(0.0, 0.0), noise_mode=L.NOISE_NONE,
@@ -498,8 +487,7 @@ def _device(device):
         "cuda", torch.cuda.current_device())
 
 
-def autotune(n, device=None, reps=6, candidates=None, method="csghmc", placed=True,
-             collect=False):
+def autotune(n, device=None, reps=6, candidates=None, method="csghmc", collect=False):
     """Pick the fastest launch geometry for an n-element sweep on this device.
 
     The update of every element is independent of the launch geometry (noise
@@ -514,7 +502,7 @@ def autotune(n, device=None, reps=6, candidates=None, method="csghmc", placed=Tr
     dev = _device(device)
     if candidates is None:
         candidates = AUTOTUNE_BY_METHOD.get(method, AUTOTUNE_CANDIDATES)
-    launch, launch_collect = _scratch_launchers(n, dev, method, placed)
+    launch, launch_collect = _scratch_launchers(n, dev, method)
 
     def pick(fn, cands):
         # round 1: every candidate; round 2: the three fastest again with twice
@@ -550,8 +538,6 @@ def autotune(n, device=None, reps=6, candidates=None, method="csghmc", placed=Tr
         res = (best, times, cbest, ctimes)
     set_launch_config(*best)
     del launch, launch_collect
-    import gc
-    gc.collect()  # the scratch state now, so that its placed set is parked for the chain
     torch.cuda.empty_cache()
     return res
 
@@ -612,6 +598,7 @@ def tune_on_state(launch, written, candidates, device, reps=4):
     import numpy as np
     saved = [w.clone() for w in written]
     prev = _ACTIVE[0]
+    ts = torch.cuda.current_stream(device)  # the stream `launch` enqueues on
 
     def measure(cfgs, k):
         out = {}
@@ -621,9 +608,9 @@ def tune_on_state(launch, written, candidates, device, reps=4):
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(k)]
             for e0, e1 in ev:
-                e0.record()
+                e0.record(ts)
                 launch()
-                e1.record()
+                e1.record(ts)
             torch.cuda.synchronize(device)
             out[cfg] = float(np.median([x.elapsed_time(y) for x, y in ev]))
             for w, s in zip(written, saved):
@@ -666,7 +653,7 @@ def prewarm(n, device=None, method="csghmc", seconds=2.5):
     return k
 
 
-def autotune_once(n, device, method, placed=True):
+def autotune_once(n, device, method):
     """autotune() (plain and collect steps) once per (n, device, method) in this
     process; later calls only re-install the cached winner.  Returns the plain
     step's geometry (collect_config: the collect step's).  BDL_AUTOTUNE=0
@@ -675,7 +662,7 @@ def autotune_once(n, device, method, placed=True):
         return None
     key = (int(n), str(device), method)
     if key not in _TUNED:
-        best, _, cbest, _ = autotune(n, device, method=method, placed=placed, collect=True)
+        best, _, cbest, _ = autotune(n, device, method=method, collect=True)
         _TUNED[key], _TUNED_COLLECT[key] = best, cbest
     else:
         set_launch_config(*_TUNED[key])

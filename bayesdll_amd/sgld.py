@@ -114,12 +114,10 @@ class Runner:
 
     # ------------------------------------------------------------------ train
     def seed_moments(self):
-        """methods/sgld.py:95-102: m1 = theta*1.0, m2 = theta**2, cnt = 1.
-        The pair is placed for the stand-alone moments sweep (flat.placed_moments)."""
-        from .flat import placed_moments
+        """methods/sgld.py:95-102: m1 = theta*1.0, m2 = theta**2, cnt = 1."""
         st = self._state()
-        self.post_theta_mom1, self.post_theta_mom2, self.moments_placement = placed_moments(
-            st.theta, need_m2=self.nst > 0)
+        self.post_theta_mom1 = torch.empty_like(st.theta)
+        self.post_theta_mom2 = torch.empty_like(st.theta) if self.nst > 0 else None
         K.moments_update(st.theta, self.post_theta_mom1, self.post_theta_mom2, L.COLLECT_MEAN_INIT,
                          div_mode=self.model.div_mode)
         self.post_theta_cnt = 1

@@ -255,7 +255,7 @@ class _StackedSampler:
         if st_big(self.state):
             # (scratch on plain allocations, as the stacked state's own vectors)
             self.state.launch_cfg = K.autotune_once(self.state.n, self.state.device,
-                                                    self.tune_method, placed=False)
+                                                    self.tune_method)
             if self.state.launch_cfg is not None:  # the collect steps' own geometry
                 self.state.collect_cfg = K.collect_config(self.state.n, self.state.device,
                                                           self.tune_method)

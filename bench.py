@@ -67,13 +67,8 @@ def parse():
                     help="skip the posterior-sample / moments sweeps after the timed region")
     ap.add_argument("--prewarm-seconds", type=float, default=0.0,
                     help="untimed back-to-back launches before the measurement (clock ramp)")
-    ap.add_argument("--placement", choices=("0", "search", "order"),
-                    default=os.environ.get("BDL_PLACEMENT", "0"),
-                    help="physical-chunk placement of the chain vectors: 0 = torch's allocator "
-                         "(the default, as for the Runners), search = the opt-in bounded chunk "
-                         "search (bayesdll_amd.placement), order = chunks in allocation order")
-    ap.add_argument("--no-placement", dest="placement", action="store_const", const="0",
-                    help="same as --placement 0")
+    ap.add_argument("--no-methods", action="store_true",
+                    help="skip the config-3 SGLD and the Adam-SGHMC lines after the timed region")
     ap.add_argument("--event-stride", type=int, default=0,
                     help="bracket every k-th timed launch (and the first of each kind) with "
                          "HIP events; 1 = all, 0 (default) = max(1, min(5, steps // 10)), i.e. "
@@ -284,7 +279,7 @@ def aux_kernels(st, reps=20):
     m1 rw, m2 rw = 20 B/elem)."""
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
-    from bayesdll_amd.flat import draw_buffer, moment_pair, placed_moments
+    from bayesdll_amd.flat import moment_pair
     n = st.n
     # the draw reads a cycle's Welford moments, allocated as the cSGHMC Runner
     # allocates them (flat.moment_pair: one allocation, two halves)
@@ -308,15 +303,8 @@ def aux_kernels(st, reps=20):
         res[name] = {"avg_ms": round(ms, 4), "bytes_per_elem": nbytes, "gbs": round(gbs, 1),
                      "frac": round(gbs / PEAK_HBM_GBS, 4)}
 
-    # the output buffer chosen as the Runners' posterior draws choose it
-    # (flat.draw_buffer: the plain allocation and two fresh ones timed)
-    out, dinfo = draw_buffer(out, lambda b: K.posterior_sample(
-        b, m1, m2, var_mode=L.VAR_WELFORD, ratio=4.0, seed=7, chain=0, step=0))
     timed("posterior_sample", 12, lambda i: K.posterior_sample(
         out, m1, m2, var_mode=L.VAR_WELFORD, ratio=4.0, seed=7, chain=0, step=i))
-    if dinfo is not None:
-        res["posterior_sample"]["out_candidates_ms"] = dinfo["torch_ms"]
-        res["posterior_sample"]["out_kept"] = dinfo["kept"]
     res["posterior_sample"]["moments"] = "flat.moment_pair"
     # the draw's own launch geometry: its tuned workgroups/CU x 4 groups
     geo = K.sample_geometry(n, st.device) or (2, 4)
@@ -325,17 +313,12 @@ def aux_kernels(st, reps=20):
         [m1, m2], [out], geo, res["posterior_sample"]["avg_ms"])
     del m1, m2, out
     # the running moments of sgld / sghmc (methods/sgld.py:95-102 seeds them
-    # from theta at burn-in), allocated as the sgld Runner allocates them:
-    # placed for this sweep (flat.placed_moments)
-    s1, s2, pinfo = placed_moments(st.theta)
+    # from theta at burn-in), two allocations as the sgld Runner makes them
+    s1, s2 = torch.empty_like(st.theta), torch.empty_like(st.theta)
     s1.copy_(st.theta)
     s2.fill_(1e-6)
     timed("moments_update", 20, lambda i: K.moments_update(
         st.theta, s1, s2, L.COLLECT_MEAN, collect_a=float(i + 1), collect_b=float(i + 2)))
-    if pinfo is not None:
-        res["moments_update"]["placement"] = {k: pinfo.get(k) for k in (
-            "allocator", "kept", "seconds", "default_ms", "chosen_ms", "untuned_torch_ms",
-            "composites_ms", "pairs_timed", "chunks_allocated", "transient_gb")}
     cfg = getattr(st, "launch_cfg", None) or (2, 4, 1)
     res["moments_update"]["mix_ceiling"] = mix_ceiling(
         [st.theta, s1, s2], [s1, s2], (cfg[0], 4), res["moments_update"]["avg_ms"])
@@ -422,60 +405,111 @@ def explore_tensor_grad_timing(st, reps=20):
     """Informational, after the timed region: the explore step reading the
     gradient as the Runners read autograd's (default "tensor" gradient mode,
     methods/csghmc.py:741-778 reads each p.grad): one fresh torch allocation
-    per parameter tensor (296 for ViT-L/32, never placed) through the per-run
-    base table, on the same theta / momentum as the timed region."""
+    per parameter tensor (296 for ViT-L/32) through the per-run base table,
+    on the same theta / momentum as the timed region.  To separate the cost of
+    the per-tensor run table from the physical placement of 296 separate
+    allocations, the same step is also timed through the same per-tensor
+    table over 296 views of the ONE flat gradient allocation the headline
+    reads (`one_allocation`)."""
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
-    grads = [st.grad[o:o + k].clone() for o, k in zip(st.offsets, st.numels)]
     flat = st.grad
-    st.use_tensor_grads(grads)
 
     def fn(i):
         K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-5, 1e-3), noise_scale=(0.0, 0.0),
                       noise_mode=L.NOISE_NONE, one_minus_alpha=1 - 0.18, prior_sig=1.0,
                       seed=0, chain=0, step=3_000_000 + i)
-    try:
-        res = kind_stats(event_times(fn, reps, warm=2), BYTES_PER_ELEM["explore"], st.n)
-    finally:
+
+    def restore():
         st.grad_mode, st.grad, st.gbase, st._untouched = "flat", flat, None, ()
         st.runs, st.nruns = st._base_runs
+
+    grads = [flat[o:o + k].clone() for o, k in zip(st.offsets, st.numels)]
+    try:
+        st.use_tensor_grads(grads)
+        res = kind_stats(event_times(fn, reps, warm=2), BYTES_PER_ELEM["explore"], st.n)
+        restore()
+        st.use_tensor_grads([flat[o:o + k] for o, k in zip(st.offsets, st.numels)])
+        one = kind_stats(event_times(fn, reps, warm=2), BYTES_PER_ELEM["explore"], st.n)
+    finally:
+        restore()
         del grads
-    res["gradients"] = f"{len(st.numels)} per-tensor torch allocations (unplaced)"
+    res["gradients"] = f"{len(st.numels)} per-tensor torch allocations"
+    res["runs"] = len(st.numels)
+    res["one_allocation"] = {k: one[k] for k in ("avg_ms", "p10_ms", "p50_ms", "p90_ms", "frac")}
     return res
 
 
-def explore_placed_timing(st, segs, readout, reps=20):
-    """Informational, after the timed region (--placement 0 runs only): the
-    explore step on a second chain state built with the opt-in physical-chunk
-    placement search (BDL_PLACEMENT=search, bayesdll_amd.placement), same
-    values and geometry as the timed state — what the opt-in buys on this box,
-    next to the default's number."""
+METHOD_LINES = {
+    # config 3 (BASELINE.json): ResNet-101 SGLD + SGD(momentum 0.5), Philox
+    # noise; sgld.py:469-484 + torch.optim.SGD: theta rw, g r, theta0 r, buf rw
+    "sgld_rn101": ("resnet101", "sgld", "sgld", 24),
+    # Adam-SGHMC + SGD(momentum 0.5) on ViT-L/32 (adam_sghmc.py:500-553 +
+    # :229): theta, v_mom, m, v, buf rw; g, theta0 r
+    "adam_vit": ("vit_l_32", "adam", "adam", 48),
+}
+
+
+def method_line(name, num_classes, rank, traffic_path, reps=20):
+    """Informational, after the timed region: the steady-state sweep of
+    another method on a fresh chain state of its named backbone (synthetic
+    theta0 ~ N(0, 0.02^2), theta = theta0 + N(0, 1e-3^2), g ~ N(0, 1e-3^2);
+    lr 1e-4 / 1e-2 on the readout, nd 0.01, N = 1840 x 1e3, SGD momentum 0.5,
+    Philox noise): one first step (the SGD buffer is created, as in a run),
+    then the launch geometry tuned on the state's own vectors at the first
+    steady-state launch, then `reps` separately bracketed launches.  With its
+    fraction of 8 TB/s, the bare access mix of its own buffers (mix_ceiling)
+    and the committed PMC bytes per launch."""
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
     from bayesdll_amd.flat import FlatState
-    prev = os.environ.get("BDL_PLACEMENT", "0")
-    os.environ["BDL_PLACEMENT"] = "search"
-    try:
-        ps = FlatState.from_segments(segs, readout, device=st.device, placement="csghmc")
-        ps.theta.copy_(st.theta)
-        ps.grad.copy_(st.grad)
-        ps.mom.copy_(st.mom)
-        ps.launch_cfg = getattr(st, "launch_cfg", None)
+    from bayesdll_amd.shapes import segments
+    backbone, method, kind, nbytes = METHOD_LINES[name]
+    segs, readout = segments(backbone, num_classes)
+    adam = method == "adam"
+    dev = torch.device("cuda", torch.cuda.current_device())
+    st = FlatState.from_segments(segs, readout, device=dev, need_prior=True,
+                                 extra=K.ADAM_EXTRA if adam else ())
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    st.prior.normal_(0.0, 0.02, generator=gen)
+    st.theta.normal_(0.0, 1e-3, generator=gen).add_(st.prior)
+    st.grad.normal_(0.0, 1e-3, generator=gen)
+    lr, lr_head, nd, N, mu = 1e-4, 1e-2, 0.01, 1840.0 * 1e3, 0.5
+    K.request_state_tuning(st, method)
 
-        def fn(i):
-            K.sgmcmc_step(ps, L.CSGHMC, lrs=(1e-5, 1e-3), noise_scale=(0.0, 0.0),
-                          noise_mode=L.NOISE_NONE, one_minus_alpha=1 - 0.18, prior_sig=1.0,
-                          seed=0, chain=0, step=4_000_000 + i)
-        res = kind_stats(event_times(fn, reps, warm=2), BYTES_PER_ELEM["explore"], st.n)
-        info = ps.placement_info or {}
-        res["placement"] = {k: info.get(k) for k in ("allocator", "kept", "seconds", "chosen_ms",
-                                                      "untuned_torch_ms", "default_ms",
-                                                      "chunks_allocated", "transient_gb")}
-        del ps
-    finally:
-        os.environ["BDL_PLACEMENT"] = prev
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
+    def fn(i, first=False):
+        kw = dict(noise_mode=L.NOISE_PHILOX, sigma2=1.0, n_data=N, mu=mu, first_step=first,
+                  momentum=True, seed=42 + rank, chain=rank, step=6_000_000 + i)
+        if adam:
+            m, v, buf = (st.extra[k] for k in K.ADAM_EXTRA)
+            K.adam_step(st, L.ADAM_SGHMC, adam_m=m, adam_v=v, sgd_buf=buf, beta1=0.9,
+                        beta2=0.999, eps=1e-8, t=i + 1, momentum_decay=0.18, nd=nd,
+                        lrs=(lr, lr_head), **kw)
+        else:
+            K.sgmcmc_step(st, L.SGLD, lrs=(lr, lr_head),
+                          noise_scale=[nd * np.sqrt(2 / (N * x)) for x in (lr, lr_head)],
+                          prior_sig=1.0, **kw)
+    fn(0, first=True)
+    res = kind_stats(event_times(lambda i: fn(i + 1), reps, warm=2), nbytes, st.n)
+    cfg = st.launch_cfg or (2, 1, 1)
+    res.update({"workload": f"{backbone} {'Adam-SGHMC' if adam else 'SGLD'} + SGD(momentum 0.5)",
+                "params": st.n, "tensors": len(segs),
+                "geometry": f"{cfg[0]}wg/cu x{cfg[1]}",
+                "tuned": (st.tuned.get("step") or {}).get("ms")})
+    try:
+        tj = json.load(open(traffic_path))
+        res["traffic"] = tj.get(backbone, {}).get(kind)
+    except Exception:  # noqa: BLE001
+        res["traffic"] = None
+    if adam:
+        m, v, buf = (st.extra[k] for k in K.ADAM_EXTRA)
+        rd = [st.theta, st.grad, st.prior, st.mom, m, v, buf]
+        wr = [st.theta, st.mom, m, v, buf]
+    else:
+        rd, wr = [st.theta, st.grad, st.prior, st.mom], [st.theta, st.mom]
+    res["mix_ceiling"] = mix_ceiling(rd, wr, cfg[:2], res["avg_ms"])
+    del st
+    torch.cuda.empty_cache()
     return res
 
 
@@ -547,9 +581,6 @@ def e2e_steps(steps, warmup, local, seed, graph=False):
 
 def main():
     a = parse()
-    # one setting for every vector of the run (chain state, draw, moments)
-    os.environ["BDL_PLACEMENT"] = a.placement
-    placed = a.placement != "0"
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(a.gpus))
     dist, rank, world, local = dist_setup(a.gpus)
@@ -585,7 +616,6 @@ def main():
     adam = a.method == "adam_sghmc"
     sgld = a.method == "sgld" or adam  # adam shares config 3's state/driver shape
     st = FlatState.from_segments(segs, readout, device=dev, need_prior=sgld,
-                                 placement=tune_method if placed else None,
                                  extra=("adam_m", "adam_v", "sgd_buf") if adam else ())
     gen = torch.Generator(device=dev).manual_seed(42 + rank)
     if sgld:  # config 3: theta0 ~ N(0, 0.02^2) (pretrained stand-in), theta = theta0 + N(0, 1e-3^2)
@@ -756,16 +786,18 @@ def main():
         for v, s0 in zip(touched, snap):
             v.copy_(s0)
         del snap
+        # the geometry each kind actually runs at (kernels._use_geometry):
+        # the tuned one, or — tuning skipped — whatever is installed
+        tuned = getattr(st, "tuned", {})
         best, cbest = st.launch_cfg, st.collect_cfg
-        if best is None or cbest is None:  # BDL_AUTOTUNE=0 / tuning skipped: the defaults
-            best = cbest = best or cbest or (2, 1, 1)
-            st.tuned = {k: dict(getattr(st, "tuned", {}).get(k, {}), ms=None)
-                        for k in ("step", "collect")}
-        launch.update({"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
-                       "candidates_ms": st.tuned["step"]["ms"],
-                       # the collect steps' own geometry (kernels._use_geometry)
-                       "collect": {"blocks_per_cu": cbest[0], "unroll": cbest[1],
-                                   "candidates_ms": st.tuned["collect"]["ms"]}})
+        launch.update({
+            "step": ({"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
+                      "candidates_ms": tuned.get("step", {}).get("ms")} if best is not None else
+                     {"untuned": tuned.get("step"), "installed": K._ACTIVE[0] or "library default"}),
+            # the collect steps' own geometry; untuned, they run at the step's
+            "collect": ({"blocks_per_cu": cbest[0], "unroll": cbest[1],
+                         "candidates_ms": tuned.get("collect", {}).get("ms")} if cbest is not None
+                        else {"untuned": tuned.get("collect"), "runs_at": "the step's geometry"})})
     for k in range(a.warmup):
         step(k)
     torch.cuda.synchronize()
@@ -857,12 +889,11 @@ def main():
                    "params": n, "tensors": len(segs), "readout": readout,
                    "cycles": a.cycles, "thin": a.thin, "beta": 0.5, "noise": "philox",
                    "parallelism": f"{world} independent chains (1/GPU)",
-                   "grad_mode": a.grad_mode, "placement": a.placement},
+                   "grad_mode": a.grad_mode, "allocator": "torch caching allocator"},
         "hbm_gbs": round(hbm_gbs * world, 1),
         "eval_collective": collective,
         "launch": launch,
         "prewarm": prewarm,
-        "placement": st.placement_info,
         "moment_buffers": moment_buffers,
         "kernels": table,
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
@@ -886,12 +917,6 @@ def main():
         ex["vs_flat_explore"] = round(ex["avg_ms"] / table["explore"]["avg_ms"], 4) \
             if "explore" in table else None
         table["explore_tensor_grad"] = dict(ex, launches=0, timed_region=False)
-    if not sgld and a.grad_mode == "flat" and a.placement == "0" and world == 1 and \
-            os.environ.get("BDL_BENCH_PLACED", "1") != "0":
-        ep = explore_placed_timing(st, segs, readout)
-        ep["vs_default_explore"] = round(ep["avg_ms"] / table["explore"]["avg_ms"], 4) \
-            if "explore" in table else None
-        table["explore_placed"] = dict(ep, launches=0, timed_region=False)
     out["methodology"] = {
         "timed_kinds": sorted(set(kinds)),
         "event_stride": timer.stride,
@@ -900,15 +925,14 @@ def main():
         "post_region_kinds": [k for k, v in table.items() if v.get("timed_region") is False],
         "since": "round 3 (rounds 1-2: every launch bracketed, the init collect inside the region)"}
     if dist is not None:
-        # every rank's own dominant-kernel time and placement (rank 0's is the
-        # roofline above): the slowest GPU sets the aggregate's wall clock
-        mine = {"rank": rank, "kernel": dominant, "avg_ms": dom["avg_ms"],
-                "placement_ms": (st.placement_info or {}).get("chosen_ms")}
+        # every rank's own dominant-kernel time (rank 0's is the roofline
+        # above): the slowest GPU sets the aggregate's wall clock
+        mine = {"rank": rank, "kernel": dominant, "avg_ms": dom["avg_ms"]}
         allr = [None] * world
         dist.all_gather_object(allr, mine)
         out["per_rank"] = [{"rank": r["rank"], "kernel": r["kernel"], "avg_ms": r["avg_ms"],
                             "frac": round(alg_bytes / (r["avg_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-                            "placement_ms": r["placement_ms"], **devices[i]}
+                            **devices[i]}
                            for i, r in enumerate(allr)]
         out["distributed"] = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
                               "device_count": devices[0]["device_count"],
@@ -923,23 +947,41 @@ def main():
                 v["traffic"] = tj.get(a.backbone, {}).get(k)
         except Exception:  # noqa: BLE001
             pass
-    # last on this state (it overwrites the vectors): the dominant kernel's
-    # access mix, bare, on the same buffers
-    cfg = st.launch_cfg if launch.get("autotuned") else (max(a.blocks_per_cu, 1),
-                                                        max(a.unroll, 1), 1)
-    tiled = getattr(st, "tiled", None) is not None
+    # last on this state (they overwrite the vectors): each kind's access mix,
+    # bare, on the same buffers — the dominant kernel's, the steady-state
+    # Welford collect's (5 reads, 4 writes, in place) and the cycle-init
+    # collect's (3 reads, 4 writes), each at its own geometry and the best of
+    # MIX_GEOMS
+    manual = (max(a.blocks_per_cu, 1), max(a.unroll, 1), 1)
+    cfg = (st.launch_cfg or manual) if launch.get("autotuned") else manual
+    ccfg = (st.collect_cfg or cfg) if launch.get("autotuned") else manual
     if not adam:
         rd = [st.theta, st.grad] + ([st.prior] if sgld else []) + [st.mom]
         out["roofline"]["mix_ceiling"] = mix_ceiling(rd, [st.theta, st.mom], cfg[:2],
                                                      dom["avg_ms"])
-    elif not tiled:
+    else:
         ex = st.extra
         out["roofline"]["mix_ceiling"] = mix_ceiling(
             [st.theta, st.grad, st.prior, st.mom, ex["adam_m"], ex["adam_v"], ex["sgd_buf"]],
             [st.theta, st.mom, ex["adam_m"], ex["adam_v"], ex["sgd_buf"]], cfg[:2], dom["avg_ms"])
+    if not sgld and m1s:
+        cm1, cm2 = m1s[max(m1s)], m2s[max(m1s)]  # the pair collect_steady ran on
+        if "collect_steady" in table:
+            table["collect_steady"]["mix_ceiling"] = mix_ceiling(
+                [st.theta, st.grad, st.mom, cm1, cm2], [st.theta, st.mom, cm1, cm2], ccfg[:2],
+                table["collect_steady"]["avg_ms"])
+        ci = (out.get("aux_kernels") or {}).get("collect_init")
+        if ci is not None:
+            ci["mix_ceiling"] = mix_ceiling([st.theta, st.grad, st.mom],
+                                            [st.theta, st.mom, cm1, cm2], cfg[:2], ci["avg_ms"])
+    del st, m1s, m2s
+    torch.cuda.empty_cache()
+    if world == 1 and not sgld and not a.no_methods:
+        # the other BASELINE configurations' sweeps, driver-timed on their own
+        # chain states (config 3: ResNet-101 SGLD; Adam-SGHMC on ViT-L/32)
+        out["methods"] = {nm: method_line(nm, a.num_classes, rank, a.traffic)
+                          for nm in METHOD_LINES}
     if world == 1 and a.e2e_steps > 0 and a.backbone == "vit_l_32" and not sgld:
-        del st, m1s, m2s
-        torch.cuda.empty_cache()
         e2e = e2e_steps(a.e2e_steps, 3, local, 42)
         e2e["fused_update_share"] = round(dom["avg_ms"] / e2e["ms_per_step"], 4)
         eg = e2e_steps(a.e2e_steps, 3, local, 42, graph=True)

@@ -20,7 +20,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 BDL_CSGHMC = 0
 BDL_NOISE_NONE, BDL_NOISE_PHILOX = 0, 2
 BDL_ATTR_HEAD, BDL_ATTR_PRIOR = 0x1, 0x2

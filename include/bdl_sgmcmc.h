@@ -61,7 +61,9 @@
 extern "C" {
 #endif
 
-#define BDL_ABI_VERSION 7
+/* v8: the Adam state-tiling fields (bdl_adam_args.tile_*) and the placement
+ * probe flag are gone (measured, not adopted: DESIGN.md §4). */
+#define BDL_ABI_VERSION 8
 
 typedef enum bdl_status {
   BDL_OK = 0,
@@ -112,11 +114,6 @@ typedef enum bdl_collect {
 #define BDL_FLAG_MOMENTUM 0x4    /* SGD momentum != 0: maintain args.mom as SGD buffer */
 #define BDL_FLAG_GRAD_READY 0x8  /* BDL_SGLD/BDL_SGHMC: grad already holds the sampler gradient
                                     (e.g. clipped after a *_GRAD call): apply the SGD step only */
-#define BDL_FLAG_PLACEMENT_PROBE 0x10 /* the same update under a separate kernel symbol
-                                       * (bdl_probe_kernel, depth 4), so the timing launches of
-                                       * buffer placement stay out of profiles of the production
-                                       * kernels; BDL_COLLECT_NONE, and (BDL_CSGHMC, NOISE_NONE)
-                                       * or (BDL_SGLD, NOISE_PHILOX) only */
 
 /* One parameter tensor in named_parameters order (host input to bdl_build_runs). */
 typedef struct bdl_segment {
@@ -235,20 +232,6 @@ typedef struct bdl_adam_args {
   float inv_temperature;
   float pad2;
   int32_t grad_is_mom;     /* 1: p.grad = v_mom (adam_csghmc); 0: g + v_mom         */
-  /* State tiling (ABI v7).  tile_log2 = 0: args.mom, adam_m, adam_v and
-   * sgd_buf are separate n-element vectors (the reference's layout).
-   * tile_log2 = L > 0: the streams named by tile_mask (bit 0 args.mom = v_mom,
-   * bit 1 adam_m, bit 2 adam_v, bit 3 sgd_buf) are interleaved in ONE
-   * allocation in tiles of 2^L float4 groups per stream, tile_streams streams
-   * per tile: element e of such a stream lives at
-   *   ptr[((e/4 >> L) * tile_streams * 2^L + (e/4 & (2^L - 1))) * 4 + e % 4]
-   * with ptr the stream's base (block + s * 4 * 2^L floats for stream slot s).
-   * One region instead of four separately allocated ones: on MI355X the
-   * seven-read / five-write sweep then no longer depends on where the
-   * allocator put four vectors. */
-  int32_t tile_log2;
-  int32_t tile_streams;
-  uint32_t tile_mask;
 } bdl_adam_args;
 
 /* Stand-alone posterior-moment update (no parameter update). */

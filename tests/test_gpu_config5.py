@@ -68,9 +68,7 @@ def _run(tmp_path, envs, extra, tag):
 @pytest.mark.timeout(900)
 def test_config5_eight_vit_chains_one_gpu(tmp_path):
     port = _free_port()
-    # torch's allocator (the default; eight concurrent placement searches on
-    # one GPU would time each other)
-    env0 = dict(os.environ, BDL_PLACEMENT="0")
+    env0 = dict(os.environ)
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env0.pop(k, None)
     envs = [dict(env0, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(WORLD),

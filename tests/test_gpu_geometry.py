@@ -80,60 +80,6 @@ def test_state_geometry_is_reinstalled():
         K.set_launch_config(0, 0, 0)
 
 
-@pytest.mark.parametrize("tile_log2", [5, 12])
-def test_adam_tiled_state_equals_separate_vectors(tile_log2):
-    """Adam's m / v / SGD buffer (and v_mom) interleaved in a flat.TiledState
-    (bdl_adam_args.tile_*, ABI v7) give the separate vectors' bits, through the
-    fast and the guarded path (ragged n, run boundaries at the end), with
-    tiles smaller than a block iteration and larger, at two geometries, with
-    Philox noise and running means."""
-    from bayesdll_amd import kernels as K
-    from bayesdll_amd.flat import TiledState
-    n = (1 << 20) + 4093
-    slots = ("mom", "adam_m", "adam_v", "sgd_buf")
-    outs = {}
-    try:
-        for layout in ("separate", "tiled3", "tiled4"):
-            for geo in ((1, 4, 1), (2, 2, 1)):
-                st, L = _state(n, 5)
-                K.set_launch_config(*geo)
-                if layout == "separate":
-                    vec = {nm: torch.zeros(n, device="cuda") for nm in slots}
-                    tile, ts = None, None
-                else:
-                    names = slots[1:] if layout == "tiled3" else slots
-                    ts = TiledState(n, names, "cuda", log2=tile_log2)
-                    vec = {nm: ts.stream(nm) if nm in names else torch.zeros(n, device="cuda")
-                           for nm in slots}
-                    tile = ts.abi(slots)
-                if ts is not None and "mom" in ts.names:
-                    ts.load("mom", st.mom)
-                else:
-                    vec["mom"].copy_(st.mom)
-                m1 = torch.zeros(n, device="cuda")
-                m2 = torch.zeros(n, device="cuda")
-                mom0 = st.mom
-                st.mom = vec["mom"]
-                for t in range(3):
-                    K.adam_step(st, L.ADAM_SGHMC, adam_m=vec["adam_m"], adam_v=vec["adam_v"],
-                                sgd_buf=vec["sgd_buf"], beta1=0.9, beta2=0.999, eps=1e-8,
-                                t=t + 1, momentum_decay=0.1, nd=1.0, lrs=(1e-3, 2e-3),
-                                noise_mode=L.NOISE_PHILOX, sigma2=1.0, n_data=100.0, mu=0.5,
-                                first_step=t == 0, momentum=True,
-                                collect=L.COLLECT_MEAN if t else L.COLLECT_NONE, mom1=m1,
-                                mom2=m2, collect_a=float(t), collect_b=float(t + 1), seed=3,
-                                chain=1, step=t, tile=tile)
-                st.mom = mom0
-                torch.cuda.synchronize()
-                flat = [v if v.dim() == 1 else v.reshape(-1)[:n] for v in vec.values()]
-                outs[(layout, geo)] = torch.cat([st.theta, m1, m2] + flat).clone()
-    finally:
-        K.set_launch_config(0, 0, 0)
-    ref = outs[("separate", (1, 4, 1))]
-    for k, o in outs.items():
-        assert torch.equal(o, ref), k
-
-
 @pytest.mark.parametrize("method", ["csghmc", "sgld"])
 def test_tuning_on_the_state_leaves_the_chain_unchanged(method):
     """kernels.request_state_tuning (the Runners' and bench.py's geometry
@@ -165,6 +111,9 @@ def test_tuning_on_the_state_leaves_the_chain_unchanged(method):
                                   noise_mode=L.NOISE_PHILOX, prior_sig=1.0, sigma2=1.0,
                                   n_data=100.0, mu=0.5, first_step=t == 0, momentum=True,
                                   seed=3, chain=1, step=t, **ck)
+                    if tune and t == 0:
+                        # a first step (SGD buffer written only) is not tuned on
+                        assert "step" in st._tune_pending and "step" not in st.tuned
             torch.cuda.synchronize()
             outs.append(torch.cat([st.theta, st.mom, m1, m2]).clone())
             if tune:

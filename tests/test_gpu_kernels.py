@@ -615,225 +615,6 @@ def test_full_size_vit_sghmc_matches_torch():
     np.testing.assert_allclose(st.theta.cpu().numpy(), th_ref.cpu().numpy(), rtol=2e-7, atol=1e-12)
 
 
-def test_placement_tuning_keeps_results_and_picks_the_fastest_set(monkeypatch):
-    """flat.placed_vectors (bayesdll_amd.placement's bounded search): theta and
-    mom are built from physical chunks mapped into one range each, every
-    chunk is timed against chunk 0, the fastest full-size candidate (chunk
-    assignments or plain torch allocations) is kept within the search's
-    bounds, the gradient stays a plain allocation, and the update itself never
-    depends on where the vectors live."""
-    from bayesdll_amd import _lib as L
-    from bayesdll_amd import kernels as K
-    from bayesdll_amd import placement as P
-    from bayesdll_amd.flat import FlatState, PLACEMENT_MIN_ELEMS
-    monkeypatch.setenv("BDL_PLACEMENT", "search")  # opt-in
-    segs = [("l0.weight", (PLACEMENT_MIN_ELEMS + 3,)), ("fc.weight", (1024,))]
-    outs = []
-    for placement in (None, "csghmc"):
-        st = FlatState.from_segments(segs, "fc", device=DEV, placement=placement)
-        if placement is None:
-            assert st.placement_info is None
-        else:
-            info = st.placement_info
-            per, cb = P.chunk_geometry(st.n)
-            assert info["chunks_per_vector"] == per == 1
-            assert 2 * per + 2 * per <= info["chunks_allocated"] <= P.MAX_CHUNKS
-            assert info["pairs_timed"] == info["chunks_allocated"] - 1 == len(info["ref_ms"])
-            assert info["chosen_ms"] == min(info["composites_ms"] + [info["untuned_torch_ms"]])
-            assert info["chosen_ms"] <= info["default_ms"]
-            assert info["allocator"] == ("torch" if info["kept"] == "torch" else "vmm"), info
-            assert info["transient_gb"] <= info["chunks_allocated"] * cb / 2**30 + 3 * 4 * st.n / 2**30
-            assert info["seconds"] < 2.0, info
-            if info["kept"] != "torch":
-                assert info["theta_chunks"] != info["mom_chunks"]
-                for v in (st.theta, st.mom):
-                    assert v.data_ptr() % (2 << 20) == 0
-            ptrs = {st.theta.data_ptr(), st.grad.data_ptr(), st.mom.data_ptr()}
-            assert len(ptrs) == 3
-            for v in (st.theta, st.grad, st.mom):
-                assert v.is_cuda and v.numel() == st.n
-                assert not v.any()  # zeroed
-        g = torch.Generator(device=DEV).manual_seed(0)
-        st.theta.normal_(0, 0.02, generator=g)
-        st.grad.normal_(0, 1e-3, generator=g)
-        st.mom.zero_()
-        for k in range(3):
-            K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-3, 1e-2), noise_scale=(1e-3, 1e-3),
-                          noise_mode=L.NOISE_PHILOX, one_minus_alpha=0.9, prior_sig=1.0,
-                          seed=5, step=k)
-        torch.cuda.synchronize()
-        outs.append((st.theta.clone(), st.mom.clone()))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-
-
-def test_chunk_mapping_lifetime():
-    """A mapped range lives as long as any tensor viewing it (parameters are
-    views into theta) and is unmapped when the last one goes; the physical
-    chunk survives its handle's release while mapped; a range freed during a
-    graph capture is unmapped after it, not inside it."""
-    import ctypes as C
-    import gc
-    from bayesdll_amd import _lib as L
-    from bayesdll_amd import placement as P
-    lib = L.lib()
-    gran = C.c_uint64()
-    L.check(lib.bdl_chunk_granularity(0, C.byref(gran)), "granularity")
-    assert gran.value > 0 and (2 << 20) % gran.value == 0
-    cb = 4 << 20
-    hs = []
-    for _ in range(2):
-        h = C.c_uint64()
-        L.check(lib.bdl_chunk_create(0, cb, C.byref(h)), "create")
-        hs.append(h.value)
-    t = P.Mapping(0, hs, cb, 2 * cb // 4).tensor()
-    for h in hs:
-        L.check(lib.bdl_chunk_release(h), "release")  # mapped: stays alive
-    t.copy_(torch.arange(t.numel(), device=DEV, dtype=torch.float32))
-    view = t[cb // 4 - 2: cb // 4 + 2].view(2, 2)  # straddles the two chunks
-    del t
-    gc.collect()
-    assert view.flatten().tolist() == [cb // 4 - 2, cb // 4 - 1, cb // 4, cb // 4 + 1]
-    # a range dropped inside a capture is queued, then unmapped after it
-    h = C.c_uint64()
-    L.check(lib.bdl_chunk_create(0, cb, C.byref(h)), "create")
-    m = P.Mapping(0, [h.value], cb, cb // 4)
-    L.check(lib.bdl_chunk_release(h.value), "release")
-    x = m.tensor()
-    del m
-    y = torch.zeros(4, device=DEV)
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        y.add_(1.0)
-        del x  # last reference: the unmap must be deferred
-        assert len(P._pending) == 1
-    graph.replay()
-    torch.cuda.synchronize()
-    P.release_pending()
-    assert not P._pending and y.tolist() == [1.0] * 4
-    del view
-
-
-def test_composites_mapped_one_after_another_do_not_alias():
-    """Placement maps and drops many composites of the same chunks.  On this
-    stack an address mapped once keeps translating to its first backing after
-    the unmap (tools/vmm_alias_repro.cpp), so bdl_vmm_map hands out fresh
-    sub-ranges of one arena and never reuses one: every composite must write
-    exactly its own chunks and get an address no earlier mapping had."""
-    import random
-    from bayesdll_amd import placement as P
-    cb = 64 << 20
-    ch = P._Chunks(0, cb)
-    ch.add(6)
-    try:
-        rng = random.Random(3)
-        seen = set()
-        _, mapped0 = P.va_reserved_bytes()
-        for _ in range(8):
-            ids = rng.sample(range(6), 4)
-            a = P.Mapping(0, [ch.handles[k] for k in ids[:2]], cb, 2 * cb // 4).tensor()
-            b = P.Mapping(0, [ch.handles[k] for k in ids[2:]], cb, 2 * cb // 4).tensor()
-            assert a.data_ptr() not in seen and b.data_ptr() not in seen
-            seen.update((a.data_ptr(), b.data_ptr()))
-            a.fill_(1.0)
-            b.fill_(2.0)
-            torch.cuda.synchronize()
-            for k, want in zip(ids, (1.0, 1.0, 2.0, 2.0)):
-                v = ch.views[k]
-                assert float(v.min()) == want and float(v.max()) == want, (ids, k)
-            del a, b
-        reserved, mapped = P.va_reserved_bytes()
-        assert mapped - mapped0 == 8 * 2 * 2 * cb and reserved >= mapped
-    finally:
-        ch.release()
-
-
-def test_scratch_sets_are_parked_for_the_chain_and_chain_sets_released(monkeypatch):
-    """(BDL_PLACEMENT=search, opt-in) The autotuner's scratch state (park=True) parks its placed set when it
-    dies, and the chain state of the same size, roles and method takes it
-    back: same addresses, no new search, zeroed, same bits from the update.
-    A chain state's own set (park=False) is unmapped when its last tensor
-    dies — a parameter view keeps it mapped until then."""
-    import functools
-    import gc
-    from bayesdll_amd import _lib as L
-    from bayesdll_amd import kernels as K
-    from bayesdll_amd import placement as P
-    from bayesdll_amd.flat import FlatState, PLACEMENT_MIN_ELEMS
-    P.release_pool()
-    # chunk composites only, so that there is a mapped set to park
-    monkeypatch.setenv("BDL_PLACEMENT", "search")  # opt-in
-    monkeypatch.setattr(P, "place", functools.partial(P.place, with_torch=False))
-    segs = [("l0.weight", (PLACEMENT_MIN_ELEMS + 5,)), ("fc.weight", (1000,))]
-
-    def run(st):
-        g = torch.Generator(device=DEV).manual_seed(3)
-        st.theta.normal_(0, 0.02, generator=g)
-        st.grad.normal_(0, 1e-3, generator=g)
-        for k in range(2):
-            K.sgmcmc_step(st, L.CSGHMC, lrs=(1e-3, 1e-2), noise_scale=(1e-3, 1e-3),
-                          noise_mode=L.NOISE_PHILOX, one_minus_alpha=0.9, prior_sig=1.0,
-                          seed=9, step=k)
-        torch.cuda.synchronize()
-        return st.theta.clone(), st.mom.clone()
-
-    scratch = FlatState.from_segments(segs, "fc", device=DEV, placement="csghmc", park=True)
-    info0 = scratch.placement_info
-    assert info0["allocator"] == "vmm" and not info0["reused"]
-    ptrs = (scratch.theta.data_ptr(), scratch.mom.data_ptr())
-    ref = run(scratch)
-    del scratch
-    gc.collect()
-    assert P.pooled_bytes() > 0
-    _, mapped0 = P.va_reserved_bytes()
-    st = FlatState.from_segments(segs, "fc", device=DEV, placement="csghmc")
-    info = st.placement_info
-    assert info["reused"] and info["chosen_ms"] == info0["chosen_ms"]
-    assert (st.theta.data_ptr(), st.mom.data_ptr()) == ptrs and P.pooled_bytes() == 0
-    assert not st.mom.any() and P.va_reserved_bytes()[1] == mapped0  # no new mapping
-    out = run(st)
-    assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1])
-    keep = st.theta[:10]  # a parameter view keeps the chain's set mapped
-    del st, out
-    gc.collect()
-    assert float(keep.sum()) == float(ref[0][:10].sum())
-    del keep
-    gc.collect()
-    assert P.pooled_bytes() == 0  # the chain's set was unmapped, not parked
-    st2 = FlatState.from_segments(segs, "fc", device=DEV, placement="csghmc")
-    assert not st2.placement_info["reused"]  # a new search
-    del st2
-    gc.collect()
-    P.release_pool()
-
-
-def test_placed_moments_change_nothing_but_the_addresses(monkeypatch):
-    """flat.placed_moments (the sgld / sghmc running moments, placed for the
-    stand-alone moments sweep): same bits as plain allocations through the
-    seeding and two running-mean updates (methods/sgld.py:95-102, :236-246)."""
-    from bayesdll_amd import _lib as L
-    from bayesdll_amd import kernels as K
-    from bayesdll_amd.flat import PLACEMENT_MIN_ELEMS, placed_moments
-    monkeypatch.setenv("BDL_PLACEMENT", "search")  # opt-in
-    n = PLACEMENT_MIN_ELEMS + 7
-    g = torch.Generator(device=DEV).manual_seed(4)
-    thetas = [torch.randn(n, device=DEV, generator=g) for _ in range(3)]
-    outs = []
-    for placed in (False, True):
-        if placed:
-            m1, m2, info = placed_moments(thetas[0])
-            assert info is not None and info["method"] == "moments"
-            assert not m1.any() and not m2.any() and m1.numel() == m2.numel() == n
-        else:
-            m1, m2 = torch.empty(n, device=DEV), torch.empty(n, device=DEV)
-        K.moments_update(thetas[0], m1, m2, L.COLLECT_MEAN_INIT)
-        for k, th in enumerate(thetas[1:], start=1):
-            K.moments_update(th, m1, m2, L.COLLECT_MEAN, collect_a=float(k), collect_b=float(k + 1))
-        torch.cuda.synchronize()
-        outs.append((m1.clone(), m2.clone()))
-        del m1, m2
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-
-
 def test_full_size_vit_csghmc_sample_and_welford_collect_bitexact():
     """The headline schedule's sample steps at full ViT-L/32 size: Philox noise
     + Welford first sample (m1 = theta, M2 = 0) then a Welford update with the
@@ -934,8 +715,8 @@ def test_moment_pair_changes_nothing_but_the_addresses(monkeypatch):
     bit for bit."""
     from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
-    from bayesdll_amd.flat import FlatState, PLACEMENT_MIN_ELEMS, moment_pair
-    segs = [("l0.weight", (PLACEMENT_MIN_ELEMS + 5,)), ("fc.weight", (1027,))]
+    from bayesdll_amd.flat import MOMENT_PAIR_MIN_ELEMS, FlatState, moment_pair
+    segs = [("l0.weight", (MOMENT_PAIR_MIN_ELEMS + 5,)), ("fc.weight", (1027,))]
     res = []
     for paired in (True, False):
         st = FlatState.from_segments(segs, "fc", device=DEV)

@@ -39,7 +39,7 @@ def _port():
 
 def run():
     os.makedirs(OUT, exist_ok=True)
-    env0 = dict(os.environ, BDL_PLACEMENT="0", TMPDIR="/tmp")
+    env0 = dict(os.environ, TMPDIR="/tmp")
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env0.pop(k, None)
     lone = PROF + ["-d", os.path.join(OUT, "lone"), "-o", "run", "--",

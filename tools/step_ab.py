@@ -1,11 +1,13 @@
 """Same-process A/B of library builds on the fused ViT-L/32 cSGHMC step
-(tooling).  One FlatState (physical-chunk placement, theta / mom on the fast
-pairing), then for every build in argv and every launch geometry, the explore
-step (theta rw, grad r, mom rw) and the Welford collect step, HIP-event mean
-over 20 launches, builds alternating A, B, C, ... for ROUNDS rounds — so a
-build's number is never a different placement's number.
+(tooling).  One FlatState, then for every build in argv and every launch
+geometry, the explore step (theta rw, grad r, mom rw) and the Welford collect
+step, HIP-event mean over 20 launches, builds alternating A, B, C, ... for
+ROUNDS rounds — so a build's number is never a different allocation's number.
 
   python tools/step_ab.py LIB [LIB ...]     (ROUNDS=4, GEOMS="1,4,1;2,1,1;1,2,1;1,4,0")
+  GRAD=tensor: the gradient read per tensor through the run / base table from
+  separate allocations (the Runners' default); GRAD=views: the same table over
+  views of the one flat gradient allocation.
 """
 import json
 import os
@@ -39,9 +41,7 @@ use(libs[0])
 segs, readout = segments(os.environ.get("BACKBONE", "vit_l_32"), 1000)
 adam = METHOD == "adam"
 sgld = METHOD == "sgld"
-st = FlatState.from_segments(segs, readout, device=dev,
-                             placement=None if os.environ.get("BDL_PLACEMENT", "0") == "0"
-                             else METHOD, need_prior=adam or sgld,
+st = FlatState.from_segments(segs, readout, device=dev, need_prior=adam or sgld,
                              extra=("adam_m", "adam_v", "sgd_buf") if adam else ())
 gen = torch.Generator(device=dev).manual_seed(1)
 st.theta.normal_(0.0, 0.02, generator=gen)
@@ -49,9 +49,13 @@ st.grad.normal_(0.0, 1e-3, generator=gen)
 m1 = st.theta.clone()
 m2 = torch.zeros_like(st.theta)
 n = st.n
-print(json.dumps({"placement": {k: (st.placement_info or {}).get(k) for k in
-                                ("allocator", "chosen_ms", "untuned_torch_ms", "kept")}}),
-      flush=True)
+GRAD = os.environ.get("GRAD", "flat")
+if GRAD == "tensor":
+    _grads = [st.grad[o:o + k].clone() for o, k in zip(st.offsets, st.numels)]
+    st.use_tensor_grads(_grads)
+elif GRAD == "views":
+    st.use_tensor_grads([st.grad[o:o + k] for o, k in zip(st.offsets, st.numels)])
+print(json.dumps({"grad": GRAD, "runs": st.nruns}), flush=True)
 lrs, alpha, N = (1e-4, 1e-2), 0.18, 1840.0
 
 

@@ -25,7 +25,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
     sys.exit(0)
 
 k = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-env = dict(os.environ, BDL_PLACEMENT="order")
+env = dict(os.environ)
 procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--child"], env=env,
                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for _ in range(k)]
 bits = []
