@@ -21,6 +21,7 @@ Noise modes (`Model.noise_mode`, or env BDL_NOISE_MODE):
 from __future__ import annotations
 
 import contextlib
+import ctypes as C
 import gc
 import os
 
@@ -57,6 +58,7 @@ def _drop_graphs(graphs):
         graphs.clear()
         release_deferred_graphs()
 MAX_GRAPHS = 4  # captured forward/backward graphs per sampler (one per input shape)
+MAX_OVERLAP_GRAPHS = 16  # with the update captured: one per (input shape, step kind)
 
 
 @contextlib.contextmanager
@@ -138,6 +140,8 @@ class FusedModelBase(nn.Module):
         self._ovl_plan = None
         self._ovl_hooks = None
         self._side = None
+        self.overlap_graph_failed = False  # the update could not be captured: eager overlap
+        self.overlap_graph_error = None
         self._state = None
         self._state_net = None
 
@@ -184,10 +188,9 @@ class FusedModelBase(nn.Module):
         return loss, out
 
     def can_overlap(self, st):
-        return (self.overlap and not self.graph and st.grad_mode == "tensor"
-                and self.noise_mode == "philox")
+        return self.overlap and st.grad_mode == "tensor" and self.noise_mode == "philox"
 
-    def forward_backward_overlapped(self, st, net, x, y, criterion, launch):
+    def forward_backward_overlapped(self, st, net, x, y, criterion, launch, kind=None):
         """Forward + backward with the fused update overlapped: the flat
         vectors are cut into ~64 MB buckets of whole tensors
         (FlatState.bucket_plan); when the last gradient of a bucket has been
@@ -199,7 +202,51 @@ class FusedModelBase(nn.Module):
         and (with philox_offset = start // 4) the same noise as one launch:
         the chain is bit-identical.  Buckets holding a parameter without a
         gradient are launched after backward, with it skipped.  Philox noise
-        and "tensor" gradients only (can_overlap)."""
+        and "tensor" gradients only (can_overlap).  In graph mode the bucket
+        launches are captured with forward and backward, one graph per `kind`
+        (the step's kernel selection), _graphed_overlapped."""
+        if self.graph and kind is not None and x.is_cuda and y.is_cuda and \
+                torch.is_grad_enabled():
+            got = self._graphed_overlapped(st, net, x, y, criterion, launch, kind)
+            if got is not None:
+                return got
+        self._ensure_ovl_plan(st)
+        _, plan, owner, need = self._ovl_plan
+        main = torch.cuda.current_stream(st.device)
+        side = self._side
+
+        def fire(bi):
+            start, end, idx = plan[bi]
+            ptrs = [0 if st.params[i].grad is None else st.params[i].grad.data_ptr() for i in idx]
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                launch(st.bucket_state(plan[bi], ptrs), start)
+
+        out = net(x)
+        loss = criterion(out, y)
+        st.zero_grad()
+        self._backward_firing(loss, plan, need, owner, fire)
+        main.wait_stream(side)
+        st.sync_grads()  # which parameters got a gradient (has_grad / noise bookkeeping)
+        return loss, out
+
+    def _backward_firing(self, loss, plan, need, owner, fire):
+        """loss.backward() with each bucket's `fire` called from the hook of
+        its last gradient; buckets not fired by then are fired after it."""
+        self._ovl = {"pending": list(need), "done": [False] * len(plan), "fire": fire,
+                     "owner": owner}
+        try:
+            loss.backward()
+        finally:
+            ctx, self._ovl = self._ovl, None
+        for bi, d in enumerate(ctx["done"]):
+            if not d:
+                ctx["done"][bi] = True
+                fire(bi)
+
+    def _ensure_ovl_plan(self, st):
         dev = st.device
         if self._ovl_plan is None or self._ovl_plan[0] is not st:
             plan = st.bucket_plan(OVERLAP_BUCKET_ELEMS)
@@ -215,35 +262,6 @@ class FusedModelBase(nn.Module):
             self._ovl_hooks = [p.register_post_accumulate_grad_hook(self._ovl_hook(i))
                                for i, p in enumerate(st.params) if st.requires_grad[i]]
             self._side = torch.cuda.Stream(dev)
-        _, plan, owner, need = self._ovl_plan
-        main = torch.cuda.current_stream(dev)
-        side = self._side
-
-        def fire(bi):
-            start, end, idx = plan[bi]
-            ptrs = [0 if st.params[i].grad is None else st.params[i].grad.data_ptr() for i in idx]
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                launch(st.bucket_state(plan[bi], ptrs), start)
-
-        out = net(x)
-        loss = criterion(out, y)
-        st.zero_grad()
-        self._ovl = {"pending": list(need), "done": [False] * len(plan), "fire": fire,
-                     "owner": owner}
-        try:
-            loss.backward()
-        finally:
-            ctx, self._ovl = self._ovl, None
-        for bi, d in enumerate(ctx["done"]):
-            if not d:
-                ctx["done"][bi] = True
-                fire(bi)
-        main.wait_stream(side)
-        st.sync_grads()  # which parameters got a gradient (has_grad / noise bookkeeping)
-        return loss, out
 
     def _ovl_hook(self, i):
         def hook(_p):
@@ -256,6 +274,177 @@ class FusedModelBase(nn.Module):
                 ctx["done"][bi] = True
                 ctx["fire"](bi)
         return hook
+
+    def _graphed_overlapped(self, st, net, x, y, criterion, launch, kind):
+        """Graph mode with the update inside the graph, overlapped with the
+        backward: the bucket launches of forward_backward_overlapped are
+        captured on the side stream (fork / join through events), so the
+        memory-bound sweep of a bucket runs beside the GEMM-bound backward of
+        the layers below it.  The step's scalars change every step (learning
+        rate, noise scale, Philox step, moment vectors, counts): before each
+        replay every bucket's kernel node is rewritten in the instantiated
+        graph (bdl_graph_redirect, hipGraphExecKernelNodeSetParams) by the
+        same `launch` call the eager path makes, so the arguments are formed
+        by one code path.  One graph per (input shape, kind), `kind` naming
+        the kernel the step selects (noise on / off, collect kind).  Same
+        kernels, same arguments, same order per bucket as eager: bit-identical
+        chains (tests/test_gpu_graph_overlap.py)."""
+        key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, net.training, id(criterion),
+               id(net), "overlap", kind)
+        g = self._graphs.get(key)
+        if g is None:
+            if len(self._graphs) >= MAX_OVERLAP_GRAPHS:
+                return None
+            g = self._capture_overlapped(st, net, x, y, criterion, launch)
+            if g is None:
+                self.overlap_graph_failed = True
+                return None
+            self._graphs[key] = g
+        self._bind_graph_grads(st, g)
+        h = L.lib()
+        ex = g["graph"].raw_cuda_graph_exec()
+        try:
+            for bi, node in enumerate(g["nodes"]):
+                L.check(h.bdl_graph_redirect(ex, node), "bdl_graph_redirect")
+                launch(g["buckets"][bi], g["plan"][bi][0])
+        except RuntimeError as e:  # a node that is not this step's kernel: eager overlap
+            del self._graphs[key]
+            _drop_graphs([g["graph"]])
+            self.overlap_graph_failed, self.overlap_graph_error = True, str(e)
+            return None
+        finally:
+            h.bdl_graph_redirect(None, None)
+        g["x"].copy_(x)
+        g["y"].copy_(y)
+        g["graph"].replay()
+        st.use_grad_table(g["table"])
+        if st._touched:
+            st._touched[:] = g["touched"]
+        return g["loss"], g["out"].detach().clone()
+
+    def _capture_overlapped(self, st, net, x, y, criterion, launch):
+        """Capture forward + backward with every bucket's update launched from
+        the post-accumulate hook of its last gradient, on the side stream.
+
+        The buckets' run / gradient-base tables are allocated BEFORE the
+        capture, from torch's ordinary pool, and filled AFTER it from the
+        graph's static gradients.  (Round 4 allocated them inside the capture,
+        from the hooks: mid-backward, the graph's private pool hands out
+        blocks that earlier nodes of the same graph use for activations, so
+        every replay's forward overwrote the table the bucket kernel then read
+        — garbage gradient bases, HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION
+        on the first replay.)  Before the graph is used, each captured node's
+        arguments are read back and checked against the bucket it launches
+        (_check_overlap_nodes)."""
+        from . import kernels as K
+        sx, sy = x.detach().clone(), y.detach().clone()
+        self._warm_up(st, net, sx, sy, criterion)
+        self._ensure_ovl_plan(st)
+        _, plan, owner, need = self._ovl_plan
+        side = self._side
+        nodes, buckets, hook_ptrs = [None] * len(plan), [None] * len(plan), [None] * len(plan)
+        sizes = [3 * len(idx) for _, _, idx in plan]
+        tables = torch.zeros(sum(sizes), dtype=torch.int64, device=st.device)  # outside the graph pool
+        views, off = [], 0
+        for k in sizes:
+            views.append(tables[off:off + k])
+            off += k
+        h = L.lib()
+
+        def fire(bi):
+            start, end, idx = plan[bi]
+            ptrs = [0 if st.params[i].grad is None else st.params[i].grad.data_ptr() for i in idx]
+            hook_ptrs[bi] = ptrs
+            bs = st.bucket_state(plan[bi], ptrs, table=views[bi])
+            main = torch.cuda.current_stream(st.device)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                launch(bs, start)
+            bs.launch_cfg = K._ACTIVE[0]  # the kernel (unroll) the node was captured with
+            buckets[bi] = bs
+
+        st.zero_grad()
+        graph = torch.cuda.CUDAGraph(keep_graph=True)  # node handles stay valid
+        with no_gc(), torch.cuda.graph(graph):
+            out = net(sx)
+            loss = criterion(out, sy)
+            self._backward_firing(loss, plan, need, owner, fire)
+            torch.cuda.current_stream(st.device).wait_stream(side)
+        raw = graph.raw_cuda_graph()
+        for bi, bs in enumerate(buckets):  # each bucket's kernel node, by kernel and range
+            node = C.c_void_p()
+            if bs is not None and h.bdl_graph_find_step_node(
+                    raw, bs.theta.data_ptr(), int(bs.n), C.byref(node)) == L.BDL_OK:
+                nodes[bi] = node.value
+        err = None
+        if any(n is None for n in nodes):
+            err = "a bucket's kernel node was not found in the captured graph"
+        elif any(p.grad is not None and (p.grad.dtype != torch.float32 or
+                                         not p.grad.is_contiguous()) for p in st.params):
+            err = "a captured gradient is not a contiguous fp32 tensor"
+        else:
+            # the tables from the graph's static gradients (the hooks saw the same)
+            static = [[0 if st.params[i].grad is None else st.params[i].grad.data_ptr()
+                       for i in idx] for _, _, idx in plan]
+            if static != hook_ptrs:
+                err = "the static gradients are not the tensors the hooks saw"
+            else:
+                host = torch.cat([st.bucket_host_table(b, p) for b, p in zip(plan, static)])
+                tables.copy_(host)
+                torch.cuda.synchronize(st.device)
+                err = self._check_overlap_nodes(st, plan, nodes, buckets, tables, host, static)
+        if err is not None:
+            self.overlap_graph_error = err
+            _drop_graphs([graph])
+            return None
+        graph.instantiate()
+        st.sync_grads()
+        out, loss = out.detach(), loss.detach()
+        self.graph_captures += 1
+        return {"graph": graph, "x": sx, "y": sy, "out": out, "loss": loss,
+                "grads": [p.grad for p in st.params], "touched": list(st._touched),
+                "table": st.grad_table(), "nodes": nodes, "buckets": buckets, "plan": plan,
+                "tables": tables}
+
+    @staticmethod
+    def _check_overlap_nodes(st, plan, nodes, buckets, tables, host, static):
+        """Before any replay: every captured bucket node's kernel arguments
+        (bdl_graph_node_step_args) point at its bucket's vectors and at the
+        table allocated outside the graph; the table on the device equals the
+        one built on the host; and every gradient base, shifted back by its
+        tensor's offset, is the address of that tensor's static gradient.
+        Returns None, or what differs."""
+        h = L.lib()
+        if not torch.equal(tables.cpu(), host):
+            return "bucket table read back differs from the host table"
+        off = 0
+        for bi, ((start, end, idx), node, bs) in enumerate(zip(plan, nodes, buckets)):
+            f = (C.c_int64 * 10)()
+            if h.bdl_graph_node_step_args(C.c_void_p(node), f, 10) != L.BDL_OK:
+                return f"bucket {bi}: node arguments unreadable"
+            want = [bs.theta.data_ptr(), 0, bs.mom.data_ptr() if bs.mom is not None else 0,
+                    bs.runs.data_ptr(), bs.gbase.data_ptr(), len(idx), int(bs.n)]
+            got = [int(v) for v in f[:7]]
+            if got != want:
+                return f"bucket {bi}: captured arguments {got} != {want}"
+            if bs.runs.data_ptr() != tables.data_ptr() + 8 * off:
+                return f"bucket {bi}: run table not in the pre-allocated block"
+            nt = len(idx)
+            for j, (i, ptr) in enumerate(zip(idx, static[bi])):
+                base = int(host[off + 2 * nt + j])
+                if ptr and base + 4 * (st.offsets[i] - start) != ptr:
+                    return f"bucket {bi} tensor {i}: gradient base does not address its .grad"
+            off += 3 * nt
+        return None
+
+    def _bind_graph_grads(self, st, g):
+        if g is not self._graph_bound or any(p.grad is not gt
+                                             for p, gt in zip(st.params, g["grads"])):
+            for p, gt in zip(st.params, g["grads"]):
+                p.grad = gt
+        self._graph_bound = g
 
     def _graphed_forward_backward(self, st, net, x, y, criterion):
         """Forward + loss + backward replayed from a captured HIP graph
@@ -283,15 +472,11 @@ class FusedModelBase(nn.Module):
                 self.graph = False
                 return None
             self._graphs[key] = g
-        if g is not self._graph_bound or any(p.grad is not gt
-                                             for p, gt in zip(st.params, g["grads"])):
-            # another shape's graph (a ragged last batch, then the next epoch's
-            # full one), an eager step or user code left other tensors in .grad:
-            # point every .grad at this graph's static gradient outputs (the
-            # update reads them through the graph's table either way)
-            for p, gt in zip(st.params, g["grads"]):
-                p.grad = gt
-        self._graph_bound = g
+        # another shape's graph (a ragged last batch, then the next epoch's
+        # full one), an eager step or user code left other tensors in .grad:
+        # point every .grad at this graph's static gradient outputs (the
+        # update reads them through the graph's table either way)
+        self._bind_graph_grads(st, g)
         g["x"].copy_(x)
         g["y"].copy_(y)
         g["graph"].replay()
@@ -322,24 +507,7 @@ class FusedModelBase(nn.Module):
 
     def _capture(self, st, net, x, y, criterion):
         sx, sy = x.detach().clone(), y.detach().clone()
-        gc.collect()  # pending garbage (old pools included) goes before the capture, not in it
-        release_deferred_graphs()
-        # warm-up passes on a side stream (library handles, autotuned kernels)
-        # must not move the network's state: keep buffers (BatchNorm running
-        # statistics) and the device RNG as they were
-        bufs = [b.detach().clone() for b in net.buffers()]
-        rng = torch.cuda.get_rng_state(st.device)
-        side = torch.cuda.Stream(st.device)
-        side.wait_stream(torch.cuda.current_stream(st.device))
-        with torch.cuda.stream(side):
-            for _ in range(2):
-                st.zero_grad()
-                criterion(net(sx), sy).backward()
-        torch.cuda.current_stream(st.device).wait_stream(side)
-        with torch.no_grad():
-            for b, c in zip(net.buffers(), bufs):
-                b.copy_(c)
-        torch.cuda.set_rng_state(rng, st.device)
+        self._warm_up(st, net, sx, sy, criterion)
         st.zero_grad()  # "tensor" mode: .grad = None, so the graph's gradients are its own
         graph = torch.cuda.CUDAGraph()
         with no_gc(), torch.cuda.graph(graph):
@@ -361,6 +529,26 @@ class FusedModelBase(nn.Module):
         return {"graph": graph, "x": sx, "y": sy, "out": out, "loss": loss,
                 "grads": [p.grad for p in st.params], "touched": list(st._touched),
                 "table": st.grad_table()}
+
+    def _warm_up(self, st, net, sx, sy, criterion):
+        gc.collect()  # pending garbage (old pools included) goes before the capture, not in it
+        release_deferred_graphs()
+        # warm-up passes on a side stream (library handles, autotuned kernels)
+        # must not move the network's state: keep buffers (BatchNorm running
+        # statistics) and the device RNG as they were
+        bufs = [b.detach().clone() for b in net.buffers()]
+        rng = torch.cuda.get_rng_state(st.device)
+        side = torch.cuda.Stream(st.device)
+        side.wait_stream(torch.cuda.current_stream(st.device))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                st.zero_grad()
+                criterion(net(sx), sy).backward()
+        torch.cuda.current_stream(st.device).wait_stream(side)
+        with torch.no_grad():
+            for b, c in zip(net.buffers(), bufs):
+                b.copy_(c)
+        torch.cuda.set_rng_state(rng, st.device)
 
     # -------------------------------------------------------------- noise
     def draw_noise(self, st):

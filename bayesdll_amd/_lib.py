@@ -96,6 +96,10 @@ EXPORTS = {
     "bdl_philox_normal": (C.c_int, [C.c_void_p, C.c_int64, C.c_uint64, C.c_uint64, C.c_uint64,
                                     C.c_void_p]),
     "bdl_set_launch_config": (C.c_int, [C.c_int32, C.c_int32, C.c_int32]),
+    "bdl_graph_find_step_node": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64,
+                                            C.POINTER(C.c_void_p)]),
+    "bdl_graph_node_step_args": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]),
+    "bdl_graph_redirect": (C.c_int, [C.c_void_p, C.c_void_p]),
     # include/bdl_measure.h
     "bdl_stream_mix": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.POINTER(C.c_void_p),
                                  C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_void_p]),

@@ -350,7 +350,8 @@ class Model(FusedModelBase):
                 st, net, x, y, criterion,
                 lambda sub, start: K.sgmcmc_step(
                     sub, L.CSGHMC, noise_mode=nm, mom1=sl(m1, start, start + sub.n),
-                    mom2=sl(m2, start, start + sub.n), philox_offset=start // 4, **kw))
+                    mom2=sl(m2, start, start + sub.n), philox_offset=start // 4, **kw),
+                kind=(nm, ckind, m2 is None))
             self.step_count += 1
             return self._result(loss, out)
         loss, out = self.forward_backward(st, net, x, y, criterion)

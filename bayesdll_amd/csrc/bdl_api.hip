@@ -32,8 +32,12 @@
 // bdl_step_{csghmc,sghmc,sgld}.hip and bdl_adam.hip (kernel instances per
 // method, compiled in parallel), this file (host entry points of the C-ABI,
 // validation, launch geometry, the clip-norm / moments / sample kernels).
+#include <algorithm>
 #include "bdl_kernels.hpp"
 #include "bdl_measure.h"
+
+#include <mutex>
+#include <vector>
 
 namespace bdl {
 namespace {
@@ -535,6 +539,14 @@ int check_runs_and_grad(const bdl_step_args* s, const char* what) {
   return BDL_OK;
 }
 
+// Graph-node binding (bdl_graph_last_node / bdl_graph_redirect): the kernel
+// node the thread's last captured step launch added, and the instantiated
+// graph + node its next step launches rewrite instead of launching.
+std::mutex g_captured_mu;
+std::vector<const void*> g_captured_funcs;  // step kernels launched into a capture
+thread_local hipGraphExec_t g_redirect_exec = nullptr;
+thread_local hipGraphNode_t g_redirect_node = nullptr;
+
 int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   if (!s) return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: null args");
   if (s->n < 0) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: n < 0");
@@ -614,12 +626,49 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   a.inv_ca = recip_or(s->inv_collect_a, s->collect_a);
   a.inv_cb = recip_or(s->inv_collect_b, s->collect_b);
 
+  if (g_redirect_exec) {
+    // the node must be a kernel node running this very kernel (checked on
+    // the graph it was instantiated from): anything else is an error here,
+    // never a launch of this kernel with another node's geometry
+    hipGraphNodeType nt = hipGraphNodeTypeEmpty;
+    hipKernelNodeParams cur{};
+    if (hipGraphNodeGetType(g_redirect_node, &nt) != hipSuccess || nt != hipGraphNodeTypeKernel ||
+        hipGraphKernelNodeGetParams(g_redirect_node, &cur) != hipSuccess ||
+        cur.func != (void*)k) {
+      (void)hipGetLastError();
+      return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: the redirect node is not this step's kernel");
+    }
+    void* kp[] = {&a};
+    hipKernelNodeParams p{};
+    p.func = (void*)k;
+    p.gridDim = dim3((unsigned)grid);
+    p.blockDim = dim3(kBlock);
+    p.sharedMemBytes = (unsigned)run_lds_bytes(s);
+    p.kernelParams = kp;
+    const hipError_t err = hipGraphExecKernelNodeSetParams(g_redirect_exec, g_redirect_node, &p);
+    if (err != hipSuccess) {
+      (void)hipGetLastError();
+      g_last_error = std::string("bdl_sgmcmc_step: graph node update failed: ") +
+                     hipGetErrorString(err);
+      return BDL_ERR_LAUNCH;
+    }
+    return BDL_OK;
+  }
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kBlock), run_lds_bytes(s), stream, a);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) {
     g_last_error = std::string("bdl_sgmcmc_step: launch failed: ") + hipGetErrorString(err);
     return BDL_ERR_LAUNCH;
   }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (stream && hipStreamIsCapturing(stream, &cs) == hipSuccess &&
+      cs == hipStreamCaptureStatusActive) {
+    std::lock_guard<std::mutex> lk(g_captured_mu);
+    if (std::find(g_captured_funcs.begin(), g_captured_funcs.end(), (const void*)k) ==
+        g_captured_funcs.end())
+      g_captured_funcs.push_back((const void*)k);
+  }
+  (void)hipGetLastError();
   return BDL_OK;
 }
 
@@ -706,6 +755,82 @@ using namespace bdl;
 extern "C" {
 
 int bdl_version(void) { return BDL_ABI_VERSION; }
+
+int bdl_graph_find_step_node(void* graph, const void* theta, int64_t n, void** node) {
+  if (!graph || !node) return fail(BDL_ERR_NULL, "bdl_graph_find_step_node: null argument");
+  *node = nullptr;
+  std::vector<const void*> funcs;
+  {
+    std::lock_guard<std::mutex> lk(g_captured_mu);
+    funcs = g_captured_funcs;
+  }
+  size_t count = 0;
+  if (hipGraphGetNodes((hipGraph_t)graph, nullptr, &count) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(BDL_ERR_ARG, "bdl_graph_find_step_node: hipGraphGetNodes failed");
+  }
+  std::vector<hipGraphNode_t> nodes(count);
+  if (count && hipGraphGetNodes((hipGraph_t)graph, nodes.data(), &count) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(BDL_ERR_ARG, "bdl_graph_find_step_node: hipGraphGetNodes failed");
+  }
+  int found = 0;
+  for (hipGraphNode_t nd : nodes) {
+    hipGraphNodeType t = hipGraphNodeTypeEmpty;
+    if (hipGraphNodeGetType(nd, &t) != hipSuccess || t != hipGraphNodeTypeKernel) continue;
+    hipKernelNodeParams p{};
+    if (hipGraphKernelNodeGetParams(nd, &p) != hipSuccess) continue;
+    // only nodes running one of our step kernels carry a KArgs to look at
+    if (std::find(funcs.begin(), funcs.end(), (const void*)p.func) == funcs.end()) continue;
+    if (!p.kernelParams || !p.kernelParams[0]) continue;
+    const KArgs* ka = (const KArgs*)p.kernelParams[0];
+    if ((const void*)ka->theta == theta && ka->n == n) {
+      *node = (void*)nd;
+      ++found;
+    }
+  }
+  (void)hipGetLastError();
+  if (found != 1) {
+    *node = nullptr;
+    return fail(BDL_ERR_ARG, "bdl_graph_find_step_node: " + std::to_string(found) +
+                                 " step nodes over this range");
+  }
+  return BDL_OK;
+}
+
+int bdl_graph_node_step_args(void* node, int64_t* out, int32_t nout) {
+  if (!node || !out) return fail(BDL_ERR_NULL, "bdl_graph_node_step_args: null argument");
+  if (nout < 10) return fail(BDL_ERR_ARG, "bdl_graph_node_step_args: out needs 10 entries");
+  hipGraphNodeType t = hipGraphNodeTypeEmpty;
+  hipKernelNodeParams p{};
+  if (hipGraphNodeGetType((hipGraphNode_t)node, &t) != hipSuccess || t != hipGraphNodeTypeKernel ||
+      hipGraphKernelNodeGetParams((hipGraphNode_t)node, &p) != hipSuccess || !p.kernelParams ||
+      !p.kernelParams[0]) {
+    (void)hipGetLastError();
+    return fail(BDL_ERR_ARG, "bdl_graph_node_step_args: not a kernel node with arguments");
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_captured_mu);
+    if (std::find(g_captured_funcs.begin(), g_captured_funcs.end(), (const void*)p.func) ==
+        g_captured_funcs.end())
+      return fail(BDL_ERR_ARG, "bdl_graph_node_step_args: the node runs no captured step kernel");
+  }
+  const KArgs* ka = (const KArgs*)p.kernelParams[0];
+  const int64_t v[10] = {(int64_t)(uintptr_t)ka->theta, (int64_t)(uintptr_t)ka->grad,
+                         (int64_t)(uintptr_t)ka->mom,   (int64_t)(uintptr_t)ka->runs,
+                         (int64_t)(uintptr_t)ka->gbase, (int64_t)ka->nruns,
+                         ka->n,                          (int64_t)ka->flags,
+                         (int64_t)(uintptr_t)ka->mom1,  (int64_t)(uintptr_t)ka->mom2};
+  for (int i = 0; i < 10; ++i) out[i] = v[i];
+  return BDL_OK;
+}
+
+int bdl_graph_redirect(void* graph_exec, void* node) {
+  if (graph_exec && !node) return fail(BDL_ERR_NULL, "bdl_graph_redirect: null node");
+  g_redirect_exec = (hipGraphExec_t)graph_exec;
+  g_redirect_node = graph_exec ? (hipGraphNode_t)node : nullptr;
+  return BDL_OK;
+}
 
 const char* bdl_last_error(void) { return g_last_error.c_str(); }
 

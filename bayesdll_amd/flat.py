@@ -385,32 +385,51 @@ class FlatState:
             out.append((start, self.n, tuple(cur)))
         return out
 
-    def bucket_state(self, bucket, ptrs):
+    def bucket_host_table(self, bucket, ptrs):
+        """The run / gradient-base table of one bucket as a CPU int64 tensor of
+        3 * (tensors in the bucket) entries, [ends, attributes | bases]: run
+        ends relative to the bucket start, gradient bases shifted so local
+        element e reads ptrs[j] + 4*(start + e - offset_j); 0 = no gradient
+        (SKIP)."""
+        start, _, idx = bucket
+        nt = len(idx)
+        host = torch.empty(3 * nt, dtype=torch.int64)
+        h = host.numpy()
+        for j, (i, ptr) in enumerate(zip(idx, ptrs)):
+            o, k = self.offsets[i], self.numels[i]
+            at = self.attrs[i] | (L.ATTR_SKIP if not ptr else 0)
+            base = ptr - 4 * o + 4 * start if ptr else 0
+            if ptr and base % 16:
+                at |= L.ATTR_GUNALIGNED
+            h[2 * j], h[2 * j + 1], h[2 * nt + j] = o + k - start, at, base
+        return host
+
+    def bucket_state(self, bucket, ptrs, table=None):
         """A launchable view of one bucket: every vector sliced to
-        [start, end), a per-tensor run table with ends relative to `start`
-        and gradient bases shifted so local element e reads
-        ptrs[j] + 4*(start + e - offset_j); launch it with
-        philox_offset = start // 4 for the whole-vector noise."""
+        [start, end), with the bucket's per-tensor run / gradient-base table
+        (bucket_host_table) on the device; launch it with philox_offset =
+        start // 4 for the whole-vector noise.  table: a device int64 tensor
+        of 3 * (tensors in the bucket) entries to point the launch at instead
+        of a cached copy of the table — left UNFILLED (the graph-mode capture
+        allocates it before the capture and fills it once the static
+        gradients exist, _base._capture_overlapped)."""
         from types import SimpleNamespace
         start, end, idx = bucket
-        key = (start, tuple(ptrs))
-        tab = self._grad_tables.get(key)
-        if tab is None:
-            nt = len(idx)
-            host = torch.empty(3 * nt, dtype=torch.int64).pin_memory()
-            h = host.numpy()
-            for j, (i, ptr) in enumerate(zip(idx, ptrs)):
-                o, k = self.offsets[i], self.numels[i]
-                at = self.attrs[i] | (L.ATTR_SKIP if not ptr else 0)
-                base = ptr - 4 * o + 4 * start if ptr else 0
-                if ptr and base % 16:
-                    at |= L.ATTR_GUNALIGNED
-                h[2 * j], h[2 * j + 1], h[2 * nt + j] = o + k - start, at, base
-            dev = host.to(self.device, non_blocking=True)
-            tab = (dev[:2 * nt].view(nt, 2), nt, dev[2 * nt:])
-            if len(self._grad_tables) >= 4 * GRAD_TABLE_CACHE:
-                self._grad_tables.pop(next(iter(self._grad_tables)))
-            self._grad_tables[key] = tab
+        nt = len(idx)
+        if table is None:
+            key = (start, tuple(ptrs))
+            tab = self._grad_tables.get(key)
+            if tab is None:
+                dev = self.bucket_host_table(bucket, ptrs).pin_memory().to(self.device,
+                                                                            non_blocking=True)
+                tab = (dev[:2 * nt].view(nt, 2), nt, dev[2 * nt:])
+                if len(self._grad_tables) >= 4 * GRAD_TABLE_CACHE:
+                    self._grad_tables.pop(next(iter(self._grad_tables)))
+                self._grad_tables[key] = tab
+        else:
+            if table.numel() != 3 * nt or table.dtype != torch.int64 or table.device != self.device:
+                raise ValueError("bucket_state: table must be 3 x (bucket tensors) int64 on the device")
+            tab = (table[:2 * nt].view(nt, 2), nt, table[2 * nt:])
         sl = (lambda v: None if v is None else v[start:end])
         return SimpleNamespace(theta=self.theta[start:end], grad=None, gbase=tab[2], runs=tab[0],
                                nruns=tab[1], mom=sl(self.mom), prior=sl(self.prior), noise=None,

@@ -547,7 +547,7 @@ def cpu_baseline(segs, readout, seconds):
                       f"randn_like noise) in {el:.1f} s on {cpu_model}"}
 
 
-def e2e_steps(steps, warmup, local, seed, graph=False):
+def e2e_steps(steps, warmup, local, seed, graph=False, overlap=False):
     """Informational: full cSGHMC steps on a real ViT-L/32 (random init,
     synthetic [16,3,224,224] batch): forward + backward (PyTorch-ROCm fp32
     autograd, gradients written into the flat buffer) + the fused update.
@@ -560,6 +560,7 @@ def e2e_steps(steps, warmup, local, seed, graph=False):
     model = csghmc.Model(ND=1840, prior_sig=1.0, momentum_decay=0.18)
     model.noise_mode = "philox"
     model.graph = graph  # forward + backward replayed from a captured HIP graph
+    model.overlap = overlap  # per-bucket update beside backward (captured too in graph mode)
     crit = torch.nn.CrossEntropyLoss()
     g = torch.Generator(device=dev).manual_seed(seed)
     x = torch.randn(16, 3, 224, 224, device=dev, generator=g)
@@ -572,9 +573,11 @@ def e2e_steps(steps, warmup, local, seed, graph=False):
         model(x, y, net, None, crit, [1e-4, 1e-2], 1.0, 0.01, should_sample=(k % 10 == 0))
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
+    ovl_graphs = sum(1 for k in model._graphs if "overlap" in k)
+    model.release_graphs()
     del net, model
     torch.cuda.empty_cache()
-    return {"steps_per_s": round(1e3 / ms, 2), "ms_per_step": round(ms, 3),
+    return {"overlap_graphs": ovl_graphs, "steps_per_s": round(1e3 / ms, 2), "ms_per_step": round(ms, 3),
             "batch": [16, 3, 224, 224], "what": "ViT-L/32 fp32 fwd+bwd (autograd) + fused cSGHMC "
             "update, loss.item() sync per step as in the reference (informational)"}
 
@@ -987,6 +990,11 @@ def main():
         eg = e2e_steps(a.e2e_steps, 3, local, 42, graph=True)
         e2e["graph_ms_per_step"] = eg["ms_per_step"]
         e2e["graph_steps_per_s"] = eg["steps_per_s"]
+        # the update captured in the graph, bucket by bucket beside backward
+        if os.environ.get("BDL_BENCH_GRAPH_OVERLAP", "0") == "1":
+            eo = e2e_steps(a.e2e_steps, 3, local, 42, graph=True, overlap=True)
+            e2e["graph_overlap_ms_per_step"] = eo["ms_per_step"]
+            e2e["graph_overlap_graphs"] = eo["overlap_graphs"]
         out["e2e"] = e2e
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not sgld:
         out["cpu_baseline"] = cpu_baseline(segs, readout, a.cpu_baseline_seconds)

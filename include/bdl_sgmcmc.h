@@ -328,6 +328,24 @@ int bdl_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t chain,
  * Process-global, not thread-safe; for tuning and tests. */
 int bdl_set_launch_config(int32_t blocks_per_cu, int32_t unroll, int32_t grid_stride);
 
+/* HIP-graph node binding, for a step captured inside a HIP graph (the
+ * graph-mode update / backward overlap, bayesdll_amd/_base.py).  No reference
+ * counterpart: the reference has no graph mode.
+ * bdl_graph_find_step_node: in a captured (not yet destroyed) graph, the one
+ * kernel node of a bdl_sgmcmc_step launched during a capture over the vector
+ * at `theta` of `n` elements (BDL_ERR_ARG unless exactly one).
+ * bdl_graph_redirect: while graph_exec is non-null, the calling
+ * thread's bdl_sgmcmc_step calls launch nothing; each rewrites `node`'s kernel
+ * arguments in the instantiated graph (hipGraphExecKernelNodeSetParams) with
+ * the step it describes, which must select the kernel the node was captured
+ * with (checked first: else BDL_ERR_ARG, nothing changed).  graph_exec = null ends the redirect. */
+int bdl_graph_find_step_node(void* graph, const void* theta, int64_t n, void** node);
+/* The arguments a captured step node launches with (a diagnostic, read
+ * before the first replay): out[0..9] = theta, grad, mom, runs, grad_base,
+ * nruns, n, flags, mom1, mom2 (pointers as integers); nout >= 10. */
+int bdl_graph_node_step_args(void* node, int64_t* out, int32_t nout);
+int bdl_graph_redirect(void* graph_exec, void* node);
+
 #ifdef __cplusplus
 }
 #endif

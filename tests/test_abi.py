@@ -24,7 +24,8 @@ def test_header_declares_expected_api():
     assert declared_functions([HEADER]) == sorted([
         "bdl_version", "bdl_last_error", "bdl_build_runs", "bdl_sgmcmc_step",
         "bdl_moments_update", "bdl_posterior_sample", "bdl_philox_normal",
-        "bdl_set_launch_config", "bdl_clip_workspace_bytes", "bdl_sgld_step_clipped", "bdl_adam_step"])
+        "bdl_set_launch_config", "bdl_clip_workspace_bytes", "bdl_sgld_step_clipped", "bdl_adam_step",
+        "bdl_graph_find_step_node", "bdl_graph_node_step_args", "bdl_graph_redirect"])
 
 
 def test_library_loads_and_exports_every_declared_symbol():
