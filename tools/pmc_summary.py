@@ -51,8 +51,8 @@ def main(tag, dest=None, backbone="vit_l_32"):
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(dst, "bench_kernel_stats.csv"))
     # the bench's timed region is the tail of the trace: the dominant kernel's
-    # last `timed` dispatches (setup launches — placement candidates, autotune
-    # — come first and would bias the stats average)
+    # last `timed` dispatches (setup launches — the autotune candidates — come
+    # first and would bias the stats average)
     timed = int(os.environ.get("TIMED_LAUNCHES", "190"))
     trace = os.path.join(src, "trace", "run_kernel_trace.csv")
     if os.path.exists(trace):
@@ -71,7 +71,8 @@ def main(tag, dest=None, backbone="vit_l_32"):
         if step_kernels:
             nm = max(step_kernels, key=lambda k: len(step_kernels[k]))
             # SKIP_LAST: launches of the same kernel after the timed region
-            # (bench.py explore_tensor_grad / explore_placed: 22 each)
+            # (bench.py explore_tensor_grad: 2 x 22, per-tensor allocations
+            # and views of the flat gradient)
             skip = int(os.environ.get("SKIP_LAST", "0"))
             durs = [d for _, d in step_kernels[nm]]
             durs = (durs[:-skip] if skip else durs)[-timed:]
@@ -98,9 +99,9 @@ def main(tag, dest=None, backbone="vit_l_32"):
                 k = kind_of(r["Kernel_Name"])
                 if k:
                     acc.setdefault(k, {}).setdefault(counter, []).append(float(r["Counter_Value"]))
-    # placement times the kernel on chunk-sized vectors (< half the full
-    # vector, bayesdll_amd.placement) before the run: keep the full-size
-    # dispatches of each kind (counter >= 0.6 x the kind's largest)
+    # keep the full-size dispatches of each kind (counter >= 0.6 x the kind's
+    # largest): smaller launches of the same kernel (tests of other sizes in
+    # the same process) would bias the mean
     for d in acc.values():
         fetch = d.get("FETCH_SIZE")
         if fetch:
@@ -111,8 +112,8 @@ def main(tag, dest=None, backbone="vit_l_32"):
             big = max(write)
             d["WRITE_SIZE"] = [v for v in write if v >= 0.6 * big]
     # the run's first step (SGD buffer created: no buffer read) is the one
-    # dispatch of its kind with clearly less FETCH; autotune / placement
-    # launches come earlier, so find it by its bytes, not its position
+    # dispatch of its kind with clearly less FETCH; autotune launches come
+    # earlier, so find it by its bytes, not its position
     for k, first in FIRST_OF.items():
         d = acc.get(k)
         if not d or "FETCH_SIZE" not in d or len(d["FETCH_SIZE"]) < 3:
