@@ -646,14 +646,24 @@ __device__ __forceinline__ void chunk_multi(const KArgs& a, const StepConst& c, 
   }
 }
 
-template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
+// Variants of a step body, fixed per launch (step_variant): the SGD step on
+// an already formed gradient (BDL_FLAG_GRAD_READY) and the clipped SGLD
+// gradient (bdl_sgld_step_clipped); kVarRuntime reads both from the launch.
+constexpr int kVarGradReady = 1, kVarClip = 2, kVarRuntime = -1;
+
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL, int VAR>
 __device__ __forceinline__ void step_body(const KArgs& a) {
   StepConst c;
   c.sgd_mom = (METHOD == BDL_SGLD) && (a.flags & BDL_FLAG_MOMENTUM);
   c.sgd_mom_read = c.sgd_mom && !(a.flags & BDL_FLAG_FIRST_STEP);
   c.has_m2 = (COLLECT != BDL_COLLECT_NONE) && (a.mom2 != nullptr);
-  c.grad_ready = (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) && (a.flags & BDL_FLAG_GRAD_READY);
-  c.clip = (METHOD == BDL_SGLD) && a.clip != nullptr;
+  if constexpr (VAR == kVarRuntime) {
+    c.grad_ready = (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) && (a.flags & BDL_FLAG_GRAD_READY);
+    c.clip = (METHOD == BDL_SGLD) && a.clip != nullptr;
+  } else {
+    c.grad_ready = (VAR & kVarGradReady) != 0;
+    c.clip = (VAR & kVarClip) != 0;
+  }
   c.clip_coef = c.clip ? a.clip[1] : 1.0f;
   c.inv_s2 = a.inv_s2;
   c.inv_nd = a.inv_nd;
@@ -700,12 +710,32 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
   report_nonfinite(a, bad);
 }
 
+// In the plain (non-collect) SGLD / SGHMC sweeps — the steps of a run — the
+// rarely taken variants get bodies of their own, chosen once per launch: a
+// runtime flag tested inside the sweep keeps what it needs live across all of
+// it (SGPR spills: 6-13 per SGLD Philox instance with runtime flags, 0 with
+// variant bodies).  The collect instances (one step in `thin`) keep the
+// runtime flags: three bodies there cost more registers than they save.
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
+__device__ __forceinline__ void step_variant(const KArgs& a) {
+  if constexpr (COLLECT != BDL_COLLECT_NONE || !(METHOD == BDL_SGLD || METHOD == BDL_SGHMC)) {
+    step_body<METHOD, NOISE, COLLECT, RECIP, UNROLL, kVarRuntime>(a);
+  } else {
+    if (a.flags & BDL_FLAG_GRAD_READY)
+      step_body<METHOD, NOISE, COLLECT, RECIP, UNROLL, kVarGradReady>(a);
+    else if (METHOD == BDL_SGLD && a.clip != nullptr)
+      step_body<METHOD, NOISE, COLLECT, RECIP, UNROLL, kVarClip>(a);
+    else
+      step_body<METHOD, NOISE, COLLECT, RECIP, UNROLL, 0>(a);
+  }
+}
+
 template <int METHOD, int NOISE, int COLLECT, int UNROLL>
 __global__ __launch_bounds__(kBlock) void bdl_step_kernel(const KArgs a) {
   if (a.flags & BDL_FLAG_RECIP_DIV)
-    step_body<METHOD, NOISE, COLLECT, true, UNROLL>(a);
+    step_variant<METHOD, NOISE, COLLECT, true, UNROLL>(a);
   else
-    step_body<METHOD, NOISE, COLLECT, false, UNROLL>(a);
+    step_variant<METHOD, NOISE, COLLECT, false, UNROLL>(a);
 }
 
 // ---------------------------------------------------------------------------
