@@ -166,7 +166,7 @@ class FusedModelBase(nn.Module):
             # (plain step, collect step) with that launch's arguments, the
             # vectors it writes restored after every candidate
             # (kernels.request_state_tuning)
-            self._state.launch_cfg = self._state.collect_cfg = None
+            self._state.launch_cfg = self._state.collect_cfg = self._state.init_cfg = None
             K.request_state_tuning(self._state, self.tune_method)
         return self._state
 

@@ -103,17 +103,20 @@ __device__ __forceinline__ f4v philox_normal4(uint64_t group, uint64_t seed, uin
 // Vector helpers: a 16-B "group" covers flat elements [4g, 4g+4).  Only the
 // very last group of a vector can be partial; it takes the guarded path.
 // ---------------------------------------------------------------------------
-// Every data-stream access is a non-temporal global access: each vector is
-// touched once per step and is far larger than the 256 MiB Infinity Cache.
-// The pointers are cast to the global address space explicitly: a gradient
-// base read from the LDS run table is a generic pointer to the compiler,
-// which would otherwise emit flat_load (counted on lgkmcnt as well as
-// vmcnt, so every LDS wait of the sweep also waited for it).
+// Every data-stream access is non-temporal: each vector is touched once per
+// step and is far larger than the 256 MiB Infinity Cache.  Stores and the
+// guarded path's scalar accesses are cast to the global address space; the
+// 16-B loads are left generic (a gradient base read from the LDS run table
+// then loads with flat_load): cast to global they ran 1-1.7 % slower in the
+// explore, Welford and SGLD sweeps, same process, builds alternating
+// (profiles/round5/ab_loads/: flat explore 1.0657 vs 1.0482 ms, per-tensor
+// gradients 1.052 vs 1.0415, collect 2.014 vs 1.997, ResNet-101 SGLD at 2 x 1
+// 0.1757 vs 0.1742).
 typedef __attribute__((address_space(1))) f4v gf4v;
 typedef __attribute__((address_space(1))) float gfloat;
 
 __device__ __forceinline__ f4v vload(const float* p) {
-  return __builtin_nontemporal_load((const gf4v*)p);
+  return __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
 }
 
 __device__ __forceinline__ void vstore(float* p, f4v v) {

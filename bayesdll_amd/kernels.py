@@ -144,20 +144,27 @@ class StepTimer:
         return out
 
 
+def launch_kind(collect):
+    """The geometry kind of a launch: "collect" for the steady-state moment
+    updates (m1 / m2 read and written), "init" for a cycle's first collect
+    (m1 / m2 only written), "step" otherwise; each is tuned on its own."""
+    if collect in (L.COLLECT_WELFORD, L.COLLECT_MEAN):
+        return "collect"
+    if collect in (L.COLLECT_WELFORD_INIT, L.COLLECT_MEAN_INIT):
+        return "init"
+    return "step"
+
+
 def _launch(state, fn, a, adam=None, written=None):
-    # the steady-state collect kinds (m1 / m2 read and written) have their own
-    # geometry; the cycle's first collect (m1 / m2 only written) runs at the
-    # step's: 1.42 ms there vs 1.48 at the Welford collect's 1 x 1
-    collect = a.collect in (L.COLLECT_WELFORD, L.COLLECT_MEAN)
+    kind = launch_kind(a.collect)
     pend = getattr(state, "_tune_pending", None)
     # a first step (SGD buffer written, not read) is not the steady-state
     # access mix: the kind stays pending until a later launch
-    if pend and written is not None and int(a.n) == int(state.n) and \
-            ("collect" if collect else "step") in pend and \
+    if pend and written is not None and int(a.n) == int(state.n) and kind in pend and \
             not (a.flags & L.FLAG_FIRST_STEP) and \
             not torch.cuda.is_current_stream_capturing():
-        _tune_kind(state, fn, collect, written)
-    _use_geometry(state, collect)
+        _tune_kind(state, fn, kind, written)
+    _use_geometry(state, kind)
     t = getattr(state, "timer", None)
     e0 = t.begin() if t is not None else None
     fn()
@@ -374,13 +381,16 @@ def restore_launch_config(packed):
     return set_launch_config((packed >> 8) & 0xFFFF, packed & 0xFF, (packed >> 24) & 0xFF)
 
 
-def _use_geometry(state, collect=False):
-    """Install the geometry tuned for this state's size (state.launch_cfg, set
-    from autotune_once; state.collect_cfg for the steps that also read and
-    update the posterior moments, when tuned) if another is active: the library's launch
-    configuration is process-wide, and a process may hold states of very
-    different sizes (e.g. a one-chain sampler and a stacked one)."""
-    cfg = getattr(state, "collect_cfg", None) if collect else None
+def _use_geometry(state, kind="step"):
+    """Install the geometry tuned for this state's size and launch kind
+    (state.launch_cfg for plain steps; state.collect_cfg for the steps that
+    also read and update the posterior moments, state.init_cfg for a cycle's
+    first collect, when tuned; else the plain step's) if another is active:
+    the library's launch configuration is process-wide, and a process may hold
+    states of very different sizes (e.g. a one-chain sampler and a stacked
+    one)."""
+    cfg = getattr(state, {"collect": "collect_cfg", "init": "init_cfg"}.get(kind, "launch_cfg"),
+                  None)
     if cfg is None:
         cfg = getattr(state, "launch_cfg", None)
     if cfg is not None and cfg != _ACTIVE[0]:
@@ -402,7 +412,9 @@ AUTOTUNE_BY_METHOD = {
     # + 1 x 1 and 3 x 4: the bare access mix of the SGLD buffers ran 1 x 1 8 %
     # ahead of the tuned 2 x 1 at ResNet-101 size, and of the explore buffers
     # 3 x 4 first at ViT-L/32 size (bench.py mix_ceiling, profiles/round4/methods/)
-    "csghmc": AUTOTUNE_CANDIDATES + ((3, 4, 1),),
+    # + 1 x 1: the bare mix of the explore buffers ran fastest there on the
+    # round-5 box (1.038 ms vs 1.064 for the kernel's tuned 1 x 4)
+    "csghmc": AUTOTUNE_CANDIDATES + ((3, 4, 1), (1, 1, 1)),
     "sgld": AUTOTUNE_CANDIDATES + ((3, 4, 1), (4, 4, 1), (1, 1, 1)),
     "adam": AUTOTUNE_CANDIDATES + ((1, 1, 1), (4, 4, 1)),
 }
@@ -559,16 +571,15 @@ def request_state_tuning(state, method):
     BDL_AUTOTUNE=0: the defaults."""
     if os.environ.get("BDL_AUTOTUNE", "1") == "0" or int(state.n) < TUNE_ON_STATE_MIN:
         return
-    state._tune_pending = {"step", "collect"}
+    state._tune_pending = {"step", "collect", "init"}
     state._tune_method = method
     state.tuned = {}
 
 
-def _tune_kind(state, fn, collect, written):
-    kind = "collect" if collect else "step"
+def _tune_kind(state, fn, kind, written):
     state._tune_pending.discard(kind)
     cands = tuple(AUTOTUNE_BY_METHOD.get(state._tune_method, AUTOTUNE_CANDIDATES))
-    if collect:
+    if kind != "step":
         cands += tuple(c for c in COLLECT_EXTRA if c not in cands)
     nf = getattr(state, "nonfinite", None)
     written = list(written) + ([nf] if nf is not None else [])
@@ -581,10 +592,7 @@ def _tune_kind(state, fn, collect, written):
                                         f"{TUNE_SNAPSHOT_FRACTION:g} x free {free >> 20} MiB"}
         return
     best, times = tune_on_state(fn, written, cands, state.device)
-    if collect:
-        state.collect_cfg = best
-    else:
-        state.launch_cfg = best
+    setattr(state, {"collect": "collect_cfg", "init": "init_cfg"}.get(kind, "launch_cfg"), best)
     state.tuned[kind] = {"best": best, "ms": {f"{c[0]}wg/cu x{c[1]}": round(t, 4)
                                               for c, t in times.items()}}
 

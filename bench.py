@@ -785,6 +785,11 @@ def main():
                               collect=L.COLLECT_WELFORD if collect else L.COLLECT_NONE,
                               mom1=m1s[cyc] if collect else None,
                               mom2=m2s[cyc] if collect else None, collect_a=3.0, **kw)
+        if not sgld and cyc is not None:  # a cycle's first collect (Welford init) too
+            K.sgmcmc_step(st, L.CSGHMC, lrs=(lr, lr_head), noise_scale=(1e-7, 1e-7),
+                          noise_mode=L.NOISE_PHILOX, one_minus_alpha=1 - alpha,
+                          prior_sig=prior_sig, collect=L.COLLECT_WELFORD_INIT, mom1=m1s[cyc],
+                          mom2=m2s[cyc], collect_a=1.0, **kw)
         torch.cuda.synchronize()
         for v, s0 in zip(touched, snap):
             v.copy_(s0)
@@ -792,7 +797,7 @@ def main():
         # the geometry each kind actually runs at (kernels._use_geometry):
         # the tuned one, or — tuning skipped — whatever is installed
         tuned = getattr(st, "tuned", {})
-        best, cbest = st.launch_cfg, st.collect_cfg
+        best, cbest, ibest = st.launch_cfg, st.collect_cfg, getattr(st, "init_cfg", None)
         launch.update({
             "step": ({"blocks_per_cu": best[0], "unroll": best[1], "grid_stride": best[2],
                       "candidates_ms": tuned.get("step", {}).get("ms")} if best is not None else
@@ -800,7 +805,11 @@ def main():
             # the collect steps' own geometry; untuned, they run at the step's
             "collect": ({"blocks_per_cu": cbest[0], "unroll": cbest[1],
                          "candidates_ms": tuned.get("collect", {}).get("ms")} if cbest is not None
-                        else {"untuned": tuned.get("collect"), "runs_at": "the step's geometry"})})
+                        else {"untuned": tuned.get("collect"), "runs_at": "the step's geometry"}),
+            # a cycle's first collect (Welford init)
+            "init": ({"blocks_per_cu": ibest[0], "unroll": ibest[1],
+                      "candidates_ms": tuned.get("init", {}).get("ms")} if ibest is not None
+                     else {"untuned": tuned.get("init"), "runs_at": "the step's geometry"})})
     for k in range(a.warmup):
         step(k)
     torch.cuda.synchronize()
@@ -975,8 +984,9 @@ def main():
                 table["collect_steady"]["avg_ms"])
         ci = (out.get("aux_kernels") or {}).get("collect_init")
         if ci is not None:
+            icfg = (getattr(st, "init_cfg", None) or cfg) if launch.get("autotuned") else manual
             ci["mix_ceiling"] = mix_ceiling([st.theta, st.grad, st.mom],
-                                            [st.theta, st.mom, cm1, cm2], cfg[:2], ci["avg_ms"])
+                                            [st.theta, st.mom, cm1, cm2], icfg[:2], ci["avg_ms"])
     del st, m1s, m2s
     torch.cuda.empty_cache()
     if world == 1 and not sgld and not a.no_methods:
