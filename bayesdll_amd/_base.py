@@ -24,6 +24,7 @@ import contextlib
 import ctypes as C
 import gc
 import os
+import time
 
 import torch
 import torch.nn as nn
@@ -97,7 +98,8 @@ def default_overlap():
     return os.environ.get("BDL_OVERLAP", "0") not in ("", "0", "false", "False")
 
 
-OVERLAP_BUCKET_ELEMS = 1 << 24  # ~64 MB of fp32 per bucket
+# elements per overlap bucket (BDL_OVERLAP_BUCKET_MB, default 64 MB of fp32)
+OVERLAP_BUCKET_ELEMS = int(float(os.environ.get("BDL_OVERLAP_BUCKET_MB", "64")) * (1 << 18))
 
 
 def default_chain():
@@ -142,6 +144,8 @@ class FusedModelBase(nn.Module):
         self._side = None
         self.overlap_graph_failed = False  # the update could not be captured: eager overlap
         self.overlap_graph_error = None
+        self.overlap_rewrite_s = 0.0  # host time rewriting captured bucket nodes
+        self.overlap_replays = 0
         self._state = None
         self._state_net = None
 
@@ -303,6 +307,7 @@ class FusedModelBase(nn.Module):
         self._bind_graph_grads(st, g)
         h = L.lib()
         ex = g["graph"].raw_cuda_graph_exec()
+        t0 = time.perf_counter()
         try:
             for bi, node in enumerate(g["nodes"]):
                 L.check(h.bdl_graph_redirect(ex, node), "bdl_graph_redirect")
@@ -314,6 +319,9 @@ class FusedModelBase(nn.Module):
             return None
         finally:
             h.bdl_graph_redirect(None, None)
+        # host time spent rewriting the bucket nodes (informational)
+        self.overlap_rewrite_s += time.perf_counter() - t0
+        self.overlap_replays += 1
         g["x"].copy_(x)
         g["y"].copy_(y)
         g["graph"].replay()

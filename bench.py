@@ -574,10 +574,14 @@ def e2e_steps(steps, warmup, local, seed, graph=False, overlap=False):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
     ovl_graphs = sum(1 for k in model._graphs if "overlap" in k)
+    rewrite_ms = (1e3 * model.overlap_rewrite_s / model.overlap_replays
+                  if getattr(model, "overlap_replays", 0) else None)
+    buckets = len(model._ovl_plan[1]) if getattr(model, "_ovl_plan", None) else None
     model.release_graphs()
     del net, model
     torch.cuda.empty_cache()
-    return {"overlap_graphs": ovl_graphs, "steps_per_s": round(1e3 / ms, 2), "ms_per_step": round(ms, 3),
+    return {"overlap_graphs": ovl_graphs, "rewrite_ms_per_step": rewrite_ms, "buckets": buckets,
+            "steps_per_s": round(1e3 / ms, 2), "ms_per_step": round(ms, 3),
             "batch": [16, 3, 224, 224], "what": "ViT-L/32 fp32 fwd+bwd (autograd) + fused cSGHMC "
             "update, loss.item() sync per step as in the reference (informational)"}
 
@@ -1005,6 +1009,8 @@ def main():
             eo = e2e_steps(a.e2e_steps, 3, local, 42, graph=True, overlap=True)
             e2e["graph_overlap_ms_per_step"] = eo["ms_per_step"]
             e2e["graph_overlap_graphs"] = eo["overlap_graphs"]
+            e2e["graph_overlap_buckets"] = eo["buckets"]
+            e2e["graph_overlap_rewrite_ms_per_step"] = eo["rewrite_ms_per_step"]
         out["e2e"] = e2e
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not sgld:
         out["cpu_baseline"] = cpu_baseline(segs, readout, a.cpu_baseline_seconds)
