@@ -7,7 +7,9 @@ ROUNDS rounds — so a build's number is never a different allocation's number.
   python tools/step_ab.py LIB [LIB ...]     (ROUNDS=4, GEOMS="1,4,1;2,1,1;1,2,1;1,4,0")
   GRAD=tensor: the gradient read per tensor through the run / base table from
   separate allocations (the Runners' default); GRAD=views: the same table over
-  views of the one flat gradient allocation.
+  views of the one flat gradient allocation; GRAD=ab: flat and per-tensor
+  gradients alternating in the same process (reported as lib name + "/flat"
+  and "/tensor").
 """
 import json
 import os
@@ -50,9 +52,22 @@ m1 = st.theta.clone()
 m2 = torch.zeros_like(st.theta)
 n = st.n
 GRAD = os.environ.get("GRAD", "flat")
+_flat = st.grad
+_grads = [st.grad[o:o + k].clone() for o, k in zip(st.offsets, st.numels)] \
+    if GRAD in ("tensor", "ab") else None
+
+
+def grad_mode(mode):
+    """Switch the state between the flat gradient and the per-tensor copies."""
+    if mode == "tensor":
+        st.use_tensor_grads(_grads)
+    else:
+        st.grad_mode, st.grad, st.gbase, st._untouched = "flat", _flat, None, ()
+        st.runs, st.nruns = st._base_runs
+
+
 if GRAD == "tensor":
-    _grads = [st.grad[o:o + k].clone() for o, k in zip(st.offsets, st.numels)]
-    st.use_tensor_grads(_grads)
+    grad_mode("tensor")
 elif GRAD == "views":
     st.use_tensor_grads([st.grad[o:o + k] for o, k in zip(st.offsets, st.numels)])
 print(json.dumps({"grad": GRAD, "runs": st.nruns}), flush=True)
@@ -107,8 +122,11 @@ def t(fn, reps=20):
 res, geoms_now = {}, []
 m2.normal_(0.0, 1e-2, generator=gen).square_()
 for r in range(rounds):
-    for path in libs:
+    for path, gm in [(p, m) for p in libs for m in (("flat", "tensor") if GRAD == "ab" else (None,))]:
         use(path)
+        if gm is not None:
+            grad_mode(gm)
+        tag = os.path.basename(path) + ("" if gm is None else "/" + gm)
         for g in geoms:
             geoms_now[:] = [g]
             K.set_launch_config(*g)
@@ -118,8 +136,8 @@ for r in range(rounds):
                 if name == "collect" and (g != geoms[0] or adam or METHOD == "draw"):
                     continue
                 ms = t(fn)
-                res.setdefault((os.path.basename(path), g, name), []).append(ms)
-                print(json.dumps({"round": r, "lib": os.path.basename(path), "geom": g,
+                res.setdefault((tag, g, name), []).append(ms)
+                print(json.dumps({"round": r, "lib": tag, "geom": g,
                                   "kernel": name, "ms": round(ms, 4),
                                   "frac": round(bpe * n / ms / 1e6 / 8000.0, 4)}), flush=True)
 for (lib, g, name), v in sorted(res.items(), key=lambda kv: (kv[0][2], np.median(kv[1]))):
