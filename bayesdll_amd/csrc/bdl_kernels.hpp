@@ -477,6 +477,22 @@ __device__ __forceinline__ void chunk_fast_dispatch(const KArgs& a, const StepCo
   }
 }
 
+// The fast iterations of one run (the cSGHMC sweep, step_body): every full
+// block iteration from gb on whose groups all lie in the run (gb + kIter <=
+// lim), with the run's attributes and gradient base resolved once — no LDS
+// access, no run search between them.  Returns the first iteration not taken.
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL, bool PRIOR, bool GR>
+__device__ __forceinline__ int64_t fast_run(const KArgs& a, const StepConst& c, int64_t gb,
+                                            int64_t lim, int64_t gstep, float eta, float ns,
+                                            float* gp, uint32_t& bad) {
+  constexpr int64_t kIter = (int64_t)kBlock * UNROLL;
+  do {
+    chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, PRIOR, GR>(a, c, gb, eta, ns, gp, bad);
+    gb += gstep;
+  } while (gb + kIter <= lim);
+  return gb;
+}
+
 // Element-wise update for the slow path: attribute-dependent branches allowed.
 template <int METHOD, int NOISE, int COLLECT, bool RECIP>
 __device__ __forceinline__ void update_elem(const KArgs& a, const StepConst& c, uint32_t attr,
@@ -697,6 +713,14 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
 
   int r = find_run_lds(a.nruns, g0 * 4);
   uint32_t bad = 0;
+  // Two loop shapes, chosen per method from same-process A/Bs
+  // (profiles/round5/ab_loop/): the cSGHMC sweep resolves a run once and
+  // loops over its full iterations with no LDS access between them (explore
+  // 1.0387 vs 1.0493 ms with the per-iteration loop); the SGLD / SGHMC sweeps
+  // keep the per-iteration run lookup, which needs fewer registers (their
+  // three fast-path variants each got a loop of their own: SGPR spills 0 ->
+  // 2-14, ResNet-101 SGLD at 2 x 1 0.1793 vs 0.1716 ms).
+  if constexpr (METHOD != BDL_CSGHMC) {
   for (int64_t gb = g0; gb < g1; gb += gstep) {
     while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
     const int64_t gend = min(gb + kIter, g1);
@@ -709,6 +733,26 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
       chunk_multi<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, r, bad);
     else
       chunk_slow<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, gend, r, bad);
+  }
+  } else {
+  for (int64_t gb = g0; gb < g1;) {
+    while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
+    const uint32_t attr = run_attr(r);
+    // the full iterations from gb on whose groups all lie in run r
+    const int64_t lim = min(min(run_end(r) >> 2, nfull), g1);
+    if (!(attr & kNoFastPath) && gb + kIter <= lim) {
+      const bool head = (attr & BDL_ATTR_HEAD) != 0;
+      gb = fast_run<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(
+          a, c, gb, lim, gstep, head ? a.lr1 : a.lr0, head ? a.ns1 : a.ns0, run_grad(a, r), bad);
+      continue;
+    }
+    const int64_t gend = min(gb + kIter, g1);
+    if (gend == gb + kIter && gend <= nfull && multi_run_ok(a.nruns, r, gend * 4))
+      chunk_multi<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, r, bad);
+    else
+      chunk_slow<METHOD, NOISE, COLLECT, RECIP, UNROLL>(a, c, gb, gend, r, bad);
+    gb += gstep;
+  }
   }
   report_nonfinite(a, bad);
 }
@@ -934,6 +978,86 @@ __device__ __forceinline__ void adam_slow(const KArgs& a, const AdamConst& c, in
 }
 
 
+// Multi-run iteration of the Adam sweep (as chunk_multi for the step sweep):
+// a full block iteration across run boundaries that multi_run_ok admits; each
+// lane takes its group's run (gradient base, lr group, prior) from the LDS
+// table, every access 16-B, all loads first.
+template <int NOISE, int COLLECT, bool RECIP, bool GRADONLY, int U>
+__device__ __forceinline__ void adam_multi(const KArgs& a, const AdamConst& c, int64_t gb, int r0,
+                                           uint32_t& bad) {
+  constexpr bool kReadMoments = (COLLECT == BDL_COLLECT_MEAN);
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+  f4v th[U], g[U], vm[U], m[U], v[U], buf[U], t0[U], ep[U], m1[U], m2[U];
+  uint32_t at[U];
+  float* gq[U];
+  int rr = r0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+    while (run_end(rr) <= e) ++rr;
+    at[u] = run_attr(rr);
+    gq[u] = run_grad(a, rr);
+    buf[u] = ep[u] = m1[u] = m2[u] = z;
+    th[u] = vload(a.theta + e);
+    g[u] = vload(gq[u] + e);
+    vm[u] = vload(a.mom + e);
+    m[u] = vload(a.adam_m + e);
+    v[u] = vload(a.adam_v + e);
+    if (!GRADONLY && c.sgd_mom_read) buf[u] = vload(a.sgd_buf + e);
+    t0[u] = vload(a.prior_mean + e);
+    if constexpr (NOISE == BDL_NOISE_BUFFER) ep[u] = vload(a.noise + e);
+    if constexpr (kReadMoments) {
+      m1[u] = vload(a.mom1 + e);
+      if (c.has_m2) m2[u] = vload(a.mom2 + e);
+    }
+  }
+  StepConst cc;  // collect_core only reads inv_ca / inv_cb
+  cc.inv_ca = c.inv_ca;
+  cc.inv_cb = c.inv_cb;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    const int64_t e = gi * 4;
+    if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = step_noise4(a, gi);
+    const float eta = (at[u] & BDL_ATTR_HEAD) ? a.lr1 : a.lr0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float xt = th[u][j], xg = g[u][j], xvm = vm[u][j], xm = m[u][j], xv = v[u][j],
+            xb = buf[u][j], x1 = m1[u][j], x2 = m2[u][j];
+      if (at[u] & BDL_ATTR_PRIOR)
+        adam_core<NOISE, RECIP, true, GRADONLY>(a, c, eta, xt, xg, xvm, xm, xv, xb, t0[u][j],
+                                                ep[u][j]);
+      else
+        adam_core<NOISE, RECIP, false, GRADONLY>(a, c, eta, xt, xg, xvm, xm, xv, xb, t0[u][j],
+                                                 ep[u][j]);
+      collect_core<COLLECT, RECIP>(a, cc, xt, x1, x2);
+      th[u][j] = xt;
+      g[u][j] = xg;
+      vm[u][j] = xvm;
+      m[u][j] = xm;
+      v[u][j] = xv;
+      buf[u][j] = xb;
+      m1[u][j] = x1;
+      m2[u][j] = x2;
+    }
+    if constexpr (GRADONLY) {
+      bad |= nonfinite4(g[u]);
+      vstore(gq[u] + e, g[u]);
+    } else {
+      bad |= nonfinite4(th[u]);
+      vstore(a.theta + e, th[u]);
+    }
+    vstore(a.mom + e, vm[u]);
+    vstore(a.adam_m + e, m[u]);
+    vstore(a.adam_v + e, v[u]);
+    if (!GRADONLY && c.sgd_mom) vstore(a.sgd_buf + e, buf[u]);
+    if constexpr (COLLECT != BDL_COLLECT_NONE) {
+      vstore(a.mom1 + e, m1[u]);
+      if (c.has_m2) vstore(a.mom2 + e, m2[u]);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Software-pipelined Adam sweep (not GRADONLY): the next block iteration's loads are issued
 // before this iteration's arithmetic, so the ~420 VALU instructions per float4
@@ -1050,7 +1174,11 @@ __device__ __forceinline__ bool adam_pipe_iter(const KArgs& a, const AdamConst& 
   const int64_t gstep = (int64_t)gridDim.x * kIter;
   if (k.gb >= ngroups) return false;
   if (!k.fast) {
-    adam_slow<NOISE, COLLECT, RECIP, false, U>(a, c, k.gb, min(k.gb + kIter, ngroups), k.r, bad);
+    const int64_t gend = min(k.gb + kIter, ngroups);
+    if (gend == k.gb + kIter && gend <= (a.n >> 2) && multi_run_ok(a.nruns, k.r, gend * 4))
+      adam_multi<NOISE, COLLECT, RECIP, false, U>(a, c, k.gb, k.r, bad);
+    else
+      adam_slow<NOISE, COLLECT, RECIP, false, U>(a, c, k.gb, gend, k.r, bad);
     k.gb += gstep;
     k.fast = adam_pipe_fast<U>(a, k.gb, k.r, k.attr);
     k.loaded = false;
@@ -1132,7 +1260,10 @@ __device__ __forceinline__ void adam_body(const KArgs& a) {
       else
         adam_fast<NOISE, COLLECT, RECIP, GRADONLY, false, U>(a, c, gb, eta, run_grad(a, r), bad);
     } else {
-      adam_slow<NOISE, COLLECT, RECIP, GRADONLY, U>(a, c, gb, gend, r, bad);
+      if (gend == gb + kIter && gend <= nfull && multi_run_ok(a.nruns, r, gend * 4))
+        adam_multi<NOISE, COLLECT, RECIP, GRADONLY, U>(a, c, gb, r, bad);
+      else
+        adam_slow<NOISE, COLLECT, RECIP, GRADONLY, U>(a, c, gb, gend, r, bad);
     }
   }
   report_nonfinite(a, bad);
