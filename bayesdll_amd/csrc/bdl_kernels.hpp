@@ -713,14 +713,15 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
 
   int r = find_run_lds(a.nruns, g0 * 4);
   uint32_t bad = 0;
-  // Two loop shapes, chosen per method from same-process A/Bs
-  // (profiles/round5/ab_loop/): the cSGHMC sweep resolves a run once and
-  // loops over its full iterations with no LDS access between them (explore
-  // 1.0387 vs 1.0493 ms with the per-iteration loop); the SGLD / SGHMC sweeps
-  // keep the per-iteration run lookup, which needs fewer registers (their
-  // three fast-path variants each got a loop of their own: SGPR spills 0 ->
-  // 2-14, ResNet-101 SGLD at 2 x 1 0.1793 vs 0.1716 ms).
-  if constexpr (METHOD != BDL_CSGHMC) {
+  // Two loop shapes, chosen per kernel from same-process A/Bs
+  // (profiles/round5/ab_loop/): the plain cSGHMC sweep (explore / sample
+  // steps) resolves a run once and loops over its full iterations with no LDS
+  // access between them (explore 1.0387 vs 1.0493 ms with the per-iteration
+  // loop); the SGLD / SGHMC sweeps and the collect steps keep the
+  // per-iteration run lookup, which needs fewer registers (with the per-run
+  // loop: SGLD SGPR spills 0 -> 2-14 and ResNet-101 SGLD at 2 x 1 0.1793 vs
+  // 0.1716 ms; cSGHMC depth-4 collects 0 -> 2-6 spills).
+  if constexpr (METHOD != BDL_CSGHMC || COLLECT != BDL_COLLECT_NONE) {
   for (int64_t gb = g0; gb < g1; gb += gstep) {
     while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
     const int64_t gend = min(gb + kIter, g1);
