@@ -644,9 +644,10 @@ def tune_on_state(launch, written, candidates, device, reps=4):
 def prewarm(n, device=None, method="csghmc", seconds=2.5):
     """Run the method's kernel back to back on scratch buffers for `seconds`
     (untimed setup before a measurement): the GPU's clocks ramp over the first
-    ~2-3 s of sustained load (tools/drift.py: 1.07 -> 1.04 ms per ViT-L/32
-    sweep), so a short measurement from idle would read the ramp, not the
-    steady state.  Returns the number of launches."""
+    ~0.8 s of sustained load (tools/drift.py, round 5: 1.058 ms per ViT-L/32
+    explore sweep in the first 0.25 s, 1.032-1.035 from ~0.8 s on), so a
+    short measurement from idle would read the ramp, not the steady state.
+    Returns the number of launches."""
     import time
     dev = _device(device)
     launch = _scratch_launcher(n, dev, method)

@@ -65,8 +65,14 @@ def parse():
                          "default with autograd)")
     ap.add_argument("--no-aux", action="store_true",
                     help="skip the posterior-sample / moments sweeps after the timed region")
-    ap.add_argument("--prewarm-seconds", type=float, default=0.0,
-                    help="untimed back-to-back launches before the measurement (clock ramp)")
+    ap.add_argument("--prewarm-seconds", type=float, default=1.0,
+                    help="untimed back-to-back launches of the method's kernel on scratch "
+                         "vectors before the state is built (setup, like the tuning): the "
+                         "explore sweep runs 1.058 ms in the first 0.25 s of sustained load, "
+                         "1.045 at 0.5-0.75 s and 1.032-1.035 from ~0.8 s on "
+                         "(tools/drift.py, profiles/round5/drift.jsonl), and the tuning plus "
+                         "the warmup steps load the GPU for only ~0.35 s before the timed "
+                         "region; 0 disables it")
     ap.add_argument("--no-methods", action="store_true",
                     help="skip the config-3 SGLD and the Adam-SGHMC lines after the timed region")
     ap.add_argument("--event-stride", type=int, default=0,
@@ -604,7 +610,9 @@ def main():
     n_all = sum(int(np.prod(s)) for _, s in segs)
     prewarm = {"seconds": a.prewarm_seconds,
                "launches": K.prewarm(n_all, local, tune_method, a.prewarm_seconds)
-               if a.prewarm_seconds > 0 else 0}
+               if a.prewarm_seconds > 0 else 0,
+               "why": "untimed setup: clock / power ramp of the first ~0.8 s of load "
+                      "(tools/drift.py)"}
     tune_on_state = False
     if a.blocks_per_cu or a.unroll or a.grid_stride >= 0:
         K.set_launch_config(a.blocks_per_cu, a.unroll, max(a.grid_stride, 0))
