@@ -65,14 +65,15 @@ def parse():
                          "default with autograd)")
     ap.add_argument("--no-aux", action="store_true",
                     help="skip the posterior-sample / moments sweeps after the timed region")
-    ap.add_argument("--prewarm-seconds", type=float, default=1.0,
+    ap.add_argument("--prewarm-seconds", type=float, default=0.0,
                     help="untimed back-to-back launches of the method's kernel on scratch "
-                         "vectors before the state is built (setup, like the tuning): the "
-                         "explore sweep runs 1.058 ms in the first 0.25 s of sustained load, "
-                         "1.045 at 0.5-0.75 s and 1.032-1.035 from ~0.8 s on "
-                         "(tools/drift.py, profiles/round5/drift.jsonl), and the tuning plus "
-                         "the warmup steps load the GPU for only ~0.35 s before the timed "
-                         "region; 0 disables it")
+                         "vectors before the state is built.  The explore sweep runs 1.058 ms "
+                         "in the first 0.25 s of sustained load and 1.032-1.035 from ~0.8 s on "
+                         "(tools/drift.py, profiles/round5/drift.jsonl), but in the driver's "
+                         "command shape (--steps 20 --warmup 5) a 1 s prewarm changed nothing "
+                         "(919.5 vs 918.2 steps/s over three fresh processes each, "
+                         "profiles/round5/prewarm_ab/): the tuning and warmup already load the "
+                         "GPU, and allocation-to-allocation spread is larger; default 0")
     ap.add_argument("--no-methods", action="store_true",
                     help="skip the config-3 SGLD and the Adam-SGHMC lines after the timed region")
     ap.add_argument("--event-stride", type=int, default=0,

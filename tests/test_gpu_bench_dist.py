@@ -34,7 +34,7 @@ def _free_port():
 
 
 BENCH_ARGS = ["--steps", "20", "--warmup", "5", "--backbone", "resnet101",
-              "--no-autotune", "--e2e-steps", "0", "--prewarm-seconds", "0"]
+              "--no-autotune", "--e2e-steps", "0"]
 
 
 # ("torchrun", 8): the driver's own N=8 command shape (torch.distributed.run
