@@ -333,7 +333,7 @@ def aux_kernels(st, reps=20):
     return res
 
 
-def collect_init_timing(st, m1s, m2s, rank, reps=5):
+def collect_init_timing(st, m1s, m2s, rank, reps=10):
     """Informational, after the timed region: the cSGHMC step that takes a
     cycle's FIRST sample (Philox noise + Welford init: m1 = theta', m2 = 0;
     methods/csghmc.py:333-337; 28 B/elem), once per cycle in a real run, on one
@@ -998,8 +998,10 @@ def main():
         ci = (out.get("aux_kernels") or {}).get("collect_init")
         if ci is not None:
             icfg = (getattr(st, "init_cfg", None) or cfg) if launch.get("autotuned") else manual
+            c0 = min(m1s)  # the pair collect_init_timing ran on (placement differs per pair)
             ci["mix_ceiling"] = mix_ceiling([st.theta, st.grad, st.mom],
-                                            [st.theta, st.mom, cm1, cm2], icfg[:2], ci["avg_ms"])
+                                            [st.theta, st.mom, m1s[c0], m2s[c0]], icfg[:2],
+                                            ci["avg_ms"])
     del st, m1s, m2s
     torch.cuda.empty_cache()
     if world == 1 and not sgld and not a.no_methods:
