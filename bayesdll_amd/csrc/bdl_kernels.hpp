@@ -119,6 +119,15 @@ __device__ __forceinline__ f4v vload(const float* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
 }
 
+// A 16-B load through the global address space: never a flat_load, so it is
+// not counted in lgkmcnt.  For loads that are in flight while the same wave
+// waits on scalar (kernarg) loads — the pipelined Adam sweep's next-iteration
+// gradient — where a flat_load would hold every such wait until its data came
+// back from HBM.
+__device__ __forceinline__ f4v gvload(const float* p) {
+  return __builtin_nontemporal_load((const gf4v*)p);
+}
+
 __device__ __forceinline__ void vstore(float* p, f4v v) {
   __builtin_nontemporal_store(v, (gf4v*)p);
 }
@@ -357,8 +366,8 @@ __device__ __forceinline__ void update_core(const KArgs& a, const StepConst& c, 
 }
 
 // Posterior moments on the updated theta (parameters_to_vector after step).
-template <int COLLECT, bool RECIP>
-__device__ __forceinline__ void collect_core(const KArgs& a, const StepConst& c, float th,
+template <int COLLECT, bool RECIP, class A>
+__device__ __forceinline__ void collect_core(const A& a, const StepConst& c, float th,
                                              float& m1, float& m2) {
   if constexpr (COLLECT == BDL_COLLECT_WELFORD_INIT) {
     m1 = th;
@@ -799,8 +808,8 @@ struct AdamConst {
   float inv_s2, inv_nd, inv_temp, inv_bc1, inv_bc2, inv_ca, inv_cb;
 };
 
-template <int NOISE, bool RECIP, bool PRIOR, bool GRADONLY>
-__device__ __forceinline__ void adam_core(const KArgs& a, const AdamConst& c, float eta, float& th,
+template <int NOISE, bool RECIP, bool PRIOR, bool GRADONLY, class A>
+__device__ __forceinline__ void adam_core(const A& a, const AdamConst& c, float eta, float& th,
                                           float& g, float& vm, float& m, float& v, float& buf,
                                           float th0, float eps) {
   const float gs = sdiv<RECIP>(g, a.temp, c.inv_temp);  // p.grad / temperature
@@ -1071,6 +1080,15 @@ __device__ __forceinline__ void adam_multi(const KArgs& a, const AdamConst& c, i
 // loop body is written twice with the roles swapped: no copies); an iteration
 // that needs the guarded path drains the pipeline.  Same per-element update as
 // adam_fast / adam_slow, so results are bit-identical.
+// Register budget (round 5): the compute re-reads the update's scalars, and
+// (BDL_PHILOX_KEYS_PER_CALL, set for this unit) the Philox inputs, from the
+// kernarg segment per iteration, and the next iteration's gradient is loaded
+// through the global address space (gvload) so those scalar loads' lgkmcnt
+// waits do not wait for it: SGPR spills 189 -> 34 in the production instance
+// <PHILOX, NONE, false, 4>; ViT-L/32 Adam-SGHMC + SGD, same process, builds
+// alternating (profiles/round5/ab_adam/): 2.5862 vs 2.6615 ms at the best
+// geometry (flat gradient), 2.6104 vs 2.6455 (per-tensor gradients).  Either
+// change alone was slower.
 // ---------------------------------------------------------------------------
 template <int U>
 struct AdamRegs {
@@ -1086,7 +1104,7 @@ __device__ __forceinline__ void adam_pipe_load(const KArgs& a, const AdamConst& 
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
     const int64_t e = gi * 4;
     R.th[u] = vload(a.theta + e);
-    R.g[u] = vload(gp + e);
+    R.g[u] = gvload(gp + e);
     R.vm[u] = vload(a.mom + e);
     R.m[u] = vload(a.adam_m + e);
     R.v[u] = vload(a.adam_v + e);
@@ -1106,9 +1124,28 @@ template <int NOISE, int COLLECT, bool RECIP, bool PRIOR, int U>
 __device__ __forceinline__ void adam_pipe_compute(const KArgs& a, const AdamConst& c, int64_t gb,
                                                   float eta, float* gp, AdamRegs<U>& R,
                                                   uint32_t& bad) {
+  // the update's scalars (Adam / SGD / prior coefficients and their
+  // reciprocals) re-read from the kernarg segment per iteration (scalar loads
+  // behind a laundered segment pointer, so they are not hoisted), like the
+  // Philox inputs (step_noise4): held in SGPRs across the sweep they spilled
+  // 92-197 SGPRs into VGPR lanes in the Philox instances, read here 24-76
+  // (tools/resource_usage.py).  The kernel's KArgs is its first argument, at
+  // offset 0 of the segment.
+  typedef __attribute__((address_space(4))) const KArgs ckargs;
+  ckargs* ap = (ckargs*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(ap));
+  const ckargs& ka = *ap;
+  AdamConst c2 = c;
+  c2.inv_s2 = ka.inv_s2;
+  c2.inv_nd = ka.inv_nd;
+  c2.inv_temp = ka.inv_temp;
+  c2.inv_bc1 = ka.inv_bc1;
+  c2.inv_bc2 = ka.inv_bc2;
+  c2.inv_ca = ka.inv_ca;
+  c2.inv_cb = ka.inv_cb;
   StepConst cc;  // collect_core only reads inv_ca / inv_cb
-  cc.inv_ca = c.inv_ca;
-  cc.inv_cb = c.inv_cb;
+  cc.inv_ca = c2.inv_ca;
+  cc.inv_cb = c2.inv_cb;
   (void)gp;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -1119,9 +1156,9 @@ __device__ __forceinline__ void adam_pipe_compute(const KArgs& a, const AdamCons
     for (int j = 0; j < 4; ++j) {
       float xt = R.th[u][j], xg = R.g[u][j], xvm = R.vm[u][j], xm = R.m[u][j], xv = R.v[u][j],
             xb = R.buf[u][j], x1 = R.m1[u][j], x2 = R.m2[u][j];
-      adam_core<NOISE, RECIP, PRIOR, false>(a, c, eta, xt, xg, xvm, xm, xv, xb, R.t0[u][j],
+      adam_core<NOISE, RECIP, PRIOR, false>(ka, c2, eta, xt, xg, xvm, xm, xv, xb, R.t0[u][j],
                                             R.ep[u][j]);
-      collect_core<COLLECT, RECIP>(a, cc, xt, x1, x2);
+      collect_core<COLLECT, RECIP>(ka, cc, xt, x1, x2);
       R.th[u][j] = xt;
       R.vm[u][j] = xvm;
       R.m[u][j] = xm;
