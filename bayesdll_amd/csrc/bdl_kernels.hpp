@@ -415,13 +415,16 @@ __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, i
     const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
     v[u] = t0[u] = ep[u] = m1[u] = m2[u] = z;
     th[u] = vload(a.theta + e);
-    // SGLD reads its gradient through the global address space: the
-    // per-call Philox inputs are scalar loads, and with the gradient as a
+    // SGLD and SGHMC read their gradient through the global address space:
+    // the per-call Philox inputs are scalar loads, and with the gradient as a
     // flat_load their lgkmcnt wait would also wait for it.  Same process,
-    // builds alternating (profiles/round5/ab_noise/): ResNet-101 SGLD equal at
-    // 2 x 1 and 4 % faster at 1 x 4, its collect 1-2.4 % and ViT-L/32's 4.3 %
-    // faster; the cSGHMC explore (no noise) ran 2.7 % slower with it.
-    if constexpr (METHOD == BDL_SGLD)
+    // builds alternating: ResNet-101 SGLD equal at 2 x 1 and 4 % faster at
+    // 1 x 4, its collect 1-2.4 % and ViT-L/32's 4.3 % faster
+    // (profiles/round5/ab_noise/); SGHMC with its keys per call as well 3.8 %
+    // (ResNet-101) and 5.3 % (ViT-L/32, per-tensor gradients) faster at the
+    // best geometry (profiles/round5/ab_sghmc/).  The cSGHMC explore (no
+    // noise) ran 2.7 % slower with it.
+    if constexpr (METHOD == BDL_SGLD || METHOD == BDL_SGHMC)
       g[u] = gvload(gp + e);
     else
       g[u] = vload(gp + e);

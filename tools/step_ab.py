@@ -38,12 +38,13 @@ def use(path):
 
 
 METHOD = os.environ.get("METHOD", "csghmc")  # or "adam" (Adam-SGHMC + SGD), "sgld" (+ SGD),
-# "draw" (the Welford posterior draw; GEOMS entries = workgroups/CU, unroll)
+# "sghmc" (+ SGD(0)), "draw" (the Welford posterior draw; GEOMS entries = workgroups/CU, unroll)
 use(libs[0])
 segs, readout = segments(os.environ.get("BACKBONE", "vit_l_32"), 1000)
 adam = METHOD == "adam"
 sgld = METHOD == "sgld"
-st = FlatState.from_segments(segs, readout, device=dev, need_prior=adam or sgld,
+sghmc = METHOD == "sghmc"
+st = FlatState.from_segments(segs, readout, device=dev, need_prior=adam or sgld or sghmc,
                              extra=("adam_m", "adam_v", "sgd_buf") if adam else ())
 gen = torch.Generator(device=dev).manual_seed(1)
 st.theta.normal_(0.0, 0.02, generator=gen)
@@ -79,6 +80,11 @@ def explore(i):
         K.posterior_sample(st.mom, m1, m2, var_mode=L.VAR_WELFORD, ratio=1.0 / 7.0, seed=3,
                            step=i, geometry=geoms_now[0][:2])
         return
+    if sghmc:  # methods/sghmc.py:482-510 + SGD(momentum 0), Philox
+        K.sgmcmc_step(st, L.SGHMC, lrs=lrs, noise_scale=(1e-3, 1e-3), noise_mode=L.NOISE_PHILOX,
+                      one_minus_alpha=1 - alpha, sigma2=1.0, n_data=N * 1e3, seed=3, chain=0,
+                      step=i)
+        return
     if sgld:  # methods/sgld.py:469-484 + SGD(momentum 0.5), Philox
         K.sgmcmc_step(st, L.SGLD, lrs=lrs, noise_scale=(1e-3, 1e-3), noise_mode=L.NOISE_PHILOX,
                       prior_sig=1.0, sigma2=1.0, n_data=N * 1e3, mu=0.5, momentum=True,
@@ -95,6 +101,12 @@ def explore(i):
 
 
 def collect(i):
+    if sghmc:  # running mean / second moment on the sample steps (sghmc.py:242-245)
+        K.sgmcmc_step(st, L.SGHMC, lrs=lrs, noise_scale=(1e-3, 1e-3), noise_mode=L.NOISE_PHILOX,
+                      one_minus_alpha=1 - alpha, sigma2=1.0, n_data=N * 1e3,
+                      collect=L.COLLECT_MEAN, mom1=m1, mom2=m2, collect_a=float(i + 1),
+                      collect_b=float(i + 2), seed=3, chain=0, step=i)
+        return
     if sgld:
         K.sgmcmc_step(st, L.SGLD, lrs=lrs, noise_scale=(1e-3, 1e-3), noise_mode=L.NOISE_PHILOX,
                       prior_sig=1.0, sigma2=1.0, n_data=N * 1e3, mu=0.5, momentum=True,
@@ -130,9 +142,10 @@ for r in range(rounds):
         for g in geoms:
             geoms_now[:] = [g]
             K.set_launch_config(*g)
-            for name, fn, bpe in ((METHOD if METHOD in ("adam", "sgld", "draw") else "explore",
-                                   explore, {"adam": 48, "sgld": 24, "draw": 12}.get(METHOD, 20)),
-                                  ("collect", collect, 40 if sgld else 36)):
+            for name, fn, bpe in ((METHOD if METHOD in ("adam", "sgld", "sghmc", "draw")
+                                   else "explore", explore,
+                                   {"adam": 48, "sgld": 24, "sghmc": 24, "draw": 12}.get(METHOD, 20)),
+                                  ("collect", collect, 40 if sgld or sghmc else 36)):
                 if name == "collect" and (g != geoms[0] or adam or METHOD == "draw"):
                     continue
                 ms = t(fn)
