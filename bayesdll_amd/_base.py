@@ -59,7 +59,10 @@ def _drop_graphs(graphs):
         graphs.clear()
         release_deferred_graphs()
 MAX_GRAPHS = 4  # captured forward/backward graphs per sampler (one per input shape)
-MAX_OVERLAP_GRAPHS = 16  # with the update captured: one per (input shape, step kind)
+# with the update captured: one per (input shape, step kind).  Each holds a
+# private pool with its own static gradients and activations (for ViT-L/32 at
+# batch 16 about 1.6 GB each), for an opt-in mode that does not pay
+MAX_OVERLAP_GRAPHS = 8
 
 
 @contextlib.contextmanager
@@ -143,6 +146,7 @@ class FusedModelBase(nn.Module):
         self._ovl_hooks = None
         self._side = None
         self.overlap_graph_failed = False  # the update could not be captured: eager overlap
+        self.overlap_captures = 0  # capture attempts of the graph-mode overlap
         self.overlap_graph_error = None
         self.overlap_rewrite_s = 0.0  # host time rewriting captured bucket nodes
         self.overlap_replays = 0
@@ -187,7 +191,8 @@ class FusedModelBase(nn.Module):
         out = net(x)
         loss = criterion(out, y)
         st.zero_grad()          # in place of net.zero_grad() (FlatState.zero_grad)
-        loss.backward()
+        with st.backward_routing():  # BDL_GRAD_ARENA=1: one reservation (arena.GradArena)
+            loss.backward()
         st.sync_grads()         # which tensors got a gradient, and where they live
         return loss, out
 
@@ -231,7 +236,8 @@ class FusedModelBase(nn.Module):
         out = net(x)
         loss = criterion(out, y)
         st.zero_grad()
-        self._backward_firing(loss, plan, need, owner, fire)
+        with st.backward_routing():
+            self._backward_firing(loss, plan, need, owner, fire)
         main.wait_stream(side)
         st.sync_grads()  # which parameters got a gradient (has_grad / noise bookkeeping)
         return loss, out
@@ -242,7 +248,7 @@ class FusedModelBase(nn.Module):
         self._ovl = {"pending": list(need), "done": [False] * len(plan), "fire": fire,
                      "owner": owner}
         try:
-            loss.backward()
+            loss.backward()  # (eager: inside st.backward_routing(), the caller's)
         finally:
             ctx, self._ovl = self._ovl, None
         for bi, d in enumerate(ctx["done"]):
@@ -293,12 +299,18 @@ class FusedModelBase(nn.Module):
         the kernel the step selects (noise on / off, collect kind).  Same
         kernels, same arguments, same order per bucket as eager: bit-identical
         chains (tests/test_gpu_graph_overlap.py)."""
+        if self.overlap_graph_failed:
+            # a capture or a node rewrite failed once: eager overlap from now
+            # on, without recapturing every step (each attempt costs two
+            # warm-up passes, a capture and a synchronisation)
+            return None
         key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype, net.training, id(criterion),
                id(net), "overlap", kind)
         g = self._graphs.get(key)
         if g is None:
             if len(self._graphs) >= MAX_OVERLAP_GRAPHS:
                 return None
+            self.overlap_captures += 1
             g = self._capture_overlapped(st, net, x, y, criterion, launch)
             if g is None:
                 self.overlap_graph_failed = True
@@ -349,6 +361,11 @@ class FusedModelBase(nn.Module):
         self._warm_up(st, net, sx, sy, criterion)
         self._ensure_ovl_plan(st)
         _, plan, owner, need = self._ovl_plan
+        if K._ACTIVE[0] is None:
+            # pin the geometry the nodes are captured with, so every replay's
+            # redirect re-installs it (bs.launch_cfg below) whatever another
+            # state installs in between
+            K.set_launch_config(*K.LIBRARY_DEFAULT)
         side = self._side
         nodes, buckets, hook_ptrs = [None] * len(plan), [None] * len(plan), [None] * len(plan)
         sizes = [3 * len(idx) for _, _, idx in plan]

@@ -103,6 +103,12 @@ EXPORTS = {
     # include/bdl_measure.h
     "bdl_stream_mix": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.POINTER(C.c_void_p),
                                  C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_void_p]),
+    # include/bdl_arena.h
+    "bdl_arena_reserve": (C.c_int, [C.c_int32, C.c_int64]),
+    "bdl_arena_alloc": (C.c_void_p, [C.c_size_t, C.c_int, C.c_void_p]),
+    "bdl_arena_free": (None, [C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]),
+    "bdl_arena_stats": (C.c_int, [C.c_int32, C.POINTER(C.c_int64), C.c_int32]),
+    "bdl_arena_contains": (C.c_int, [C.c_int32, C.c_void_p, C.c_int64]),
 }
 
 _lib = None

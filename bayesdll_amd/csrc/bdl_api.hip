@@ -539,13 +539,22 @@ int check_runs_and_grad(const bdl_step_args* s, const char* what) {
   return BDL_OK;
 }
 
-// Graph-node binding (bdl_graph_last_node / bdl_graph_redirect): the kernel
-// node the thread's last captured step launch added, and the instantiated
-// graph + node its next step launches rewrite instead of launching.
+// Graph-node binding (bdl_graph_find_step_node / bdl_graph_redirect): the
+// step kernels launched into a capture (to recognise their nodes), and the
+// instantiated graph + node the thread's next bdl_sgmcmc_step rewrites
+// instead of launching.  While a redirect is set, every other launching entry
+// point refuses (no_redirect): their launches would go to the stream, mixed
+// with node rewrites.
 std::mutex g_captured_mu;
 std::vector<const void*> g_captured_funcs;  // step kernels launched into a capture
 thread_local hipGraphExec_t g_redirect_exec = nullptr;
 thread_local hipGraphNode_t g_redirect_node = nullptr;
+
+int no_redirect(const char* what) {
+  if (!g_redirect_exec) return BDL_OK;
+  return fail(BDL_ERR_ARG, std::string(what) + ": a graph redirect is active (bdl_graph_redirect); "
+              "only bdl_sgmcmc_step rewrites a node");
+}
 
 int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
   if (!s) return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: null args");
@@ -748,6 +757,10 @@ MixKernel pick_mix(int nr, int nw, int unroll) {
 }
 
 }  // namespace
+
+// errors of the other host translation units (bdl_arena.hip)
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+
 }  // namespace bdl
 
 using namespace bdl;
@@ -890,6 +903,7 @@ int64_t bdl_clip_workspace_bytes(int64_t n) {
 }
 
 int bdl_sgld_step_clipped(const bdl_step_args* s, float max_norm, void* workspace, void* stream) {
+  if (const int rc = no_redirect("bdl_sgld_step_clipped")) return rc;
   if (!s) return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: null args");
   if (!workspace) return fail(BDL_ERR_NULL, "bdl_sgld_step_clipped: null workspace");
   if (!aligned16(workspace)) return fail(BDL_ERR_ALIGN, "bdl_sgld_step_clipped: workspace not 16-B aligned");
@@ -958,6 +972,7 @@ int bdl_sgld_step_clipped(const bdl_step_args* s, float max_norm, void* workspac
 }
 
 int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream) {
+  if (const int rc = no_redirect("bdl_adam_step")) return rc;
   if (!s || !ad) return fail(BDL_ERR_NULL, "bdl_adam_step: null args");
   if (s->method != BDL_ADAM_SGHMC && s->method != BDL_ADAM_SGHMC_GRAD)
     return fail(BDL_ERR_ARG, "bdl_adam_step: method must be BDL_ADAM_SGHMC or BDL_ADAM_SGHMC_GRAD");
@@ -1049,6 +1064,7 @@ int bdl_adam_step(const bdl_step_args* s, const bdl_adam_args* ad, void* stream)
 }
 
 int bdl_moments_update(const bdl_moments_args* m, void* stream) {
+  if (const int rc = no_redirect("bdl_moments_update")) return rc;
   if (!m) return fail(BDL_ERR_NULL, "bdl_moments_update: null args");
   if (m->n < 0 || m->collect < BDL_COLLECT_WELFORD_INIT || m->collect > BDL_COLLECT_MEAN)
     return fail(BDL_ERR_ARG, "bdl_moments_update: bad n or collect mode");
@@ -1072,6 +1088,7 @@ int bdl_moments_update(const bdl_moments_args* m, void* stream) {
 }
 
 int bdl_posterior_sample(const bdl_sample_args* s, void* stream) {
+  if (const int rc = no_redirect("bdl_posterior_sample")) return rc;
   if (!s) return fail(BDL_ERR_NULL, "bdl_posterior_sample: null args");
   if (s->n < 0 || s->var_mode < BDL_VAR_GIVEN || s->var_mode > BDL_VAR_WELFORD ||
       (s->noise_mode != BDL_NOISE_BUFFER && s->noise_mode != BDL_NOISE_PHILOX))
@@ -1110,6 +1127,7 @@ int bdl_posterior_sample(const bdl_sample_args* s, void* stream) {
 int bdl_stream_mix(const float* const* reads, int32_t nreads, float* const* writes,
                    int32_t nwrites, int64_t n, int32_t blocks_per_cu, int32_t unroll,
                    void* stream) {
+  if (const int rc = no_redirect("bdl_stream_mix")) return rc;
   if (!reads || !writes) return fail(BDL_ERR_NULL, "bdl_stream_mix: null stream list");
   if (n < 0 || blocks_per_cu < 1 || blocks_per_cu > 16)
     return fail(BDL_ERR_ARG, "bdl_stream_mix: n >= 0 and blocks_per_cu in [1, 16]");
@@ -1146,6 +1164,7 @@ int bdl_stream_mix(const float* const* reads, int32_t nreads, float* const* writ
 
 int bdl_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t chain, uint64_t step,
                       void* stream) {
+  if (const int rc = no_redirect("bdl_philox_normal")) return rc;
   if (n < 0) return fail(BDL_ERR_ARG, "bdl_philox_normal: n < 0");
   if (n == 0) return BDL_OK;
   if (!out) return fail(BDL_ERR_NULL, "bdl_philox_normal: null out");

@@ -30,12 +30,14 @@ on the device for the kernels.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 
 import numpy as np
 import torch
 
 from . import _lib as L
+from .arena import default_grad_arena
 
 
 def segment_attrs(names, readout_name, bias, requires_grad):
@@ -136,6 +138,13 @@ class FlatState:
         self.grad = vecs["grad"].zero_() if self.grad_mode == "flat" else None
         self.gbase = None  # device per-run gradient bases ("tensor" mode)
         self._bind_grads()
+        # "tensor" mode with BDL_GRAD_ARENA=1: the backward allocates the
+        # gradients from one reservation (arena.GradArena, wrapped around
+        # loss.backward() by backward_routing; opt-in)
+        self.arena = None
+        if self.grad_mode == "tensor" and default_grad_arena():
+            from .arena import GradArena
+            self.arena = GradArena(dev, 4 * self.n)
 
         self.mom = vecs["mom"].zero_() if need_mom else None
         self.prior = None
@@ -204,6 +213,7 @@ class FlatState:
         self.theta = vecs["theta"] if init is None else init
         self.grad_mode = "flat"
         self.gbase = None
+        self.arena = None
         self._grad_tables = {}
         self._untouched = ()
         self.grad = vecs["grad"].zero_()
@@ -252,6 +262,13 @@ class FlatState:
             if ptr is not None and (p.grad is None or p.grad.data_ptr() != ptr):
                 self._bind_grads()
                 break
+
+    def backward_routing(self):
+        """Context for `loss.backward()`: with a gradient arena, every
+        allocation of the backward pass comes from its one reservation."""
+        if self.arena is None:
+            return contextlib.nullcontext()
+        return self.arena.routing()
 
     def sync_grads(self):
         """After backward: if user code replaced a .grad, copy it into the flat

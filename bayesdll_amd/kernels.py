@@ -368,6 +368,7 @@ def philox_normal(n, seed, chain, step, device="cuda"):
 
 
 _ACTIVE = [None]  # the geometry last installed through set_launch_config (None: defaults)
+LIBRARY_DEFAULT = (2, 1, 1)  # what the library launches with before any set_launch_config
 
 
 def set_launch_config(blocks_per_cu=0, unroll=0, grid_stride=0):

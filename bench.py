@@ -411,14 +411,17 @@ def collect_steady_timing(st, m1s, m2s, spc, rank, reps=12):
 def explore_tensor_grad_timing(st, reps=20):
     """Informational, after the timed region: the explore step reading the
     gradient as the Runners read autograd's (default "tensor" gradient mode,
-    methods/csghmc.py:741-778 reads each p.grad): one fresh torch allocation
-    per parameter tensor (296 for ViT-L/32) through the per-run base table,
-    on the same theta / momentum as the timed region.  To separate the cost of
-    the per-tensor run table from the physical placement of 296 separate
-    allocations, the same step is also timed through the same per-tensor
-    table over 296 views of the ONE flat gradient allocation the headline
-    reads (`one_allocation`)."""
+    methods/csghmc.py:741-778 reads each p.grad): one gradient tensor per
+    parameter tensor (296 for ViT-L/32) through the per-run base table, on the
+    same theta / momentum as the timed region, allocated in backward order
+    (last tensor first) from torch's default pool, as the Runners' backward
+    leaves them.  For comparison, the same 296 tensors from the gradient
+    arena's pool (`arena`: arena.GradArena, one reservation, the Runners'
+    BDL_GRAD_ARENA=1), and the same per-tensor table over 296 views of the ONE
+    flat gradient allocation the headline reads (`one_allocation`: the table's
+    own cost, no placement difference)."""
     from bayesdll_amd import _lib as L
+    from bayesdll_amd import arena as A
     from bayesdll_amd import kernels as K
     flat = st.grad
 
@@ -431,19 +434,38 @@ def explore_tensor_grad_timing(st, reps=20):
         st.grad_mode, st.grad, st.gbase, st._untouched = "flat", flat, None, ()
         st.runs, st.nruns = st._base_runs
 
-    grads = [flat[o:o + k].clone() for o, k in zip(st.offsets, st.numels)]
-    try:
-        st.use_tensor_grads(grads)
-        res = kind_stats(event_times(fn, reps, warm=2), BYTES_PER_ELEM["explore"], st.n)
+    def backward_order(alloc):
+        out = [None] * len(st.numels)
+        for i in reversed(range(len(st.numels))):
+            o, k = st.offsets[i], st.numels[i]
+            out[i] = alloc(flat[o:o + k])
+        return out
+
+    def timed(grads):
         restore()
-        st.use_tensor_grads([flat[o:o + k] for o, k in zip(st.offsets, st.numels)])
-        one = kind_stats(event_times(fn, reps, warm=2), BYTES_PER_ELEM["explore"], st.n)
+        st.use_tensor_grads(grads)
+        return kind_stats(event_times(fn, reps, warm=2), BYTES_PER_ELEM["explore"], st.n)
+
+    keys = ("avg_ms", "p10_ms", "p50_ms", "p90_ms", "frac")
+    try:
+        grads = backward_order(lambda v: v.clone())
+        res = timed(grads)
+        del grads
+        arena = A.GradArena(st.device, 4 * st.n)
+        with arena.routing():
+            grads = backward_order(lambda v: v.clone())
+        inside = all(A.contains(st.device, g) for g in grads)
+        ar = timed(grads)
+        del grads
+        one = timed([flat[o:o + k] for o, k in zip(st.offsets, st.numels)])
     finally:
         restore()
-        del grads
-    res["gradients"] = f"{len(st.numels)} per-tensor torch allocations"
+    del arena
+    res["gradients"] = (f"{len(st.numels)} per-tensor allocations from torch's default pool, "
+                        "backward order (as the Runners' backward leaves them)")
     res["runs"] = len(st.numels)
-    res["one_allocation"] = {k: one[k] for k in ("avg_ms", "p10_ms", "p50_ms", "p90_ms", "frac")}
+    res["arena"] = dict({k: ar[k] for k in keys}, in_arena=inside)
+    res["one_allocation"] = {k: one[k] for k in keys}
     return res
 
 
@@ -554,41 +576,67 @@ def cpu_baseline(segs, readout, seconds):
                       f"randn_like noise) in {el:.1f} s on {cpu_model}"}
 
 
-def e2e_steps(steps, warmup, local, seed, graph=False, overlap=False):
+def e2e_steps(steps, warmup, local, seed, graph=False, overlap=False, arena=False):
     """Informational: full cSGHMC steps on a real ViT-L/32 (random init,
     synthetic [16,3,224,224] batch): forward + backward (PyTorch-ROCm fp32
-    autograd, gradients written into the flat buffer) + the fused update.
-    Returns ms/step and the fused kernel's share."""
+    autograd; in eager mode with arena=True the gradients come from the
+    gradient arena, BDL_GRAD_ARENA=1) + the fused update, reading autograd's
+    per-tensor gradients.
+    Returns ms/step and the fused update's own mean launch time on those
+    gradients (HIP events on every launch after the warm-up)."""
     import bayesdll_amd.csghmc as csghmc
+    from bayesdll_amd import kernels as K
     from bayesdll_amd.backbones import backbone
     dev = torch.device("cuda", local)
-    torch.manual_seed(seed)
-    net = backbone("vit_l_32", 1000).to(dev)
-    model = csghmc.Model(ND=1840, prior_sig=1.0, momentum_decay=0.18)
-    model.noise_mode = "philox"
-    model.graph = graph  # forward + backward replayed from a captured HIP graph
-    model.overlap = overlap  # per-bucket update beside backward (captured too in graph mode)
-    crit = torch.nn.CrossEntropyLoss()
-    g = torch.Generator(device=dev).manual_seed(seed)
-    x = torch.randn(16, 3, 224, 224, device=dev, generator=g)
-    y = torch.randint(0, 1000, (16,), device=dev, generator=g)
-    for k in range(warmup):
-        model(x, y, net, None, crit, [1e-4, 1e-2], 1.0, 0.01, should_sample=(k % 2 == 0))
+    prev = os.environ.get("BDL_GRAD_ARENA")
+    os.environ["BDL_GRAD_ARENA"] = "1" if arena else "0"
+    try:
+        torch.manual_seed(seed)
+        net = backbone("vit_l_32", 1000).to(dev)
+        model = csghmc.Model(ND=1840, prior_sig=1.0, momentum_decay=0.18)
+        model.noise_mode = "philox"
+        model.graph = graph  # forward + backward replayed from a captured HIP graph
+        model.overlap = overlap  # per-bucket update beside backward (captured too in graph mode)
+        crit = torch.nn.CrossEntropyLoss()
+        g = torch.Generator(device=dev).manual_seed(seed)
+        x = torch.randn(16, 3, 224, 224, device=dev, generator=g)
+        y = torch.randint(0, 1000, (16,), device=dev, generator=g)
+        for k in range(warmup):
+            model(x, y, net, None, crit, [1e-4, 1e-2], 1.0, 0.01, should_sample=(k % 2 == 0))
+    finally:
+        if prev is None:
+            os.environ.pop("BDL_GRAD_ARENA", None)
+        else:
+            os.environ["BDL_GRAD_ARENA"] = prev
     torch.cuda.synchronize()
+    st = model.flat
+    in_arena = None
+    if st.arena is not None:
+        from bayesdll_amd import arena as A
+        in_arena = all(p.grad is None or A.contains(dev, p.grad) for p in st.params)
     t0 = time.perf_counter()
     for k in range(steps):
         model(x, y, net, None, crit, [1e-4, 1e-2], 1.0, 0.01, should_sample=(k % 10 == 0))
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
+    # the update alone on the Runner's own gradients, after the timed steps
+    # (HIP events around each launch; 9 explore + 1 sample step per 10, 20 B/elem)
+    st.timer = K.StepTimer(1)
+    for k in range(min(steps, 20)):
+        model(x, y, net, None, crit, [1e-4, 1e-2], 1.0, 0.01, should_sample=(k % 10 == 0))
+    upd = st.timer.summary()
+    st.timer = None
     ovl_graphs = sum(1 for k in model._graphs if "overlap" in k)
     rewrite_ms = (1e3 * model.overlap_rewrite_s / model.overlap_replays
                   if getattr(model, "overlap_replays", 0) else None)
     buckets = len(model._ovl_plan[1]) if getattr(model, "_ovl_plan", None) else None
     model.release_graphs()
-    del net, model
+    del net, model, st
     torch.cuda.empty_cache()
     return {"overlap_graphs": ovl_graphs, "rewrite_ms_per_step": rewrite_ms, "buckets": buckets,
             "steps_per_s": round(1e3 / ms, 2), "ms_per_step": round(ms, 3),
+            "update_ms": round(upd["avg_ms"], 4) if upd.get("timed") else None,
+            "grad_arena": arena and not graph, "grads_in_arena": in_arena,
             "batch": [16, 3, 224, 224], "what": "ViT-L/32 fp32 fwd+bwd (autograd) + fused cSGHMC "
             "update, loss.item() sync per step as in the reference (informational)"}
 
@@ -1012,9 +1060,15 @@ def main():
     if world == 1 and a.e2e_steps > 0 and a.backbone == "vit_l_32" and not sgld:
         e2e = e2e_steps(a.e2e_steps, 3, local, 42)
         e2e["fused_update_share"] = round(dom["avg_ms"] / e2e["ms_per_step"], 4)
+        if e2e["update_ms"] and "explore" in table:
+            e2e["update_vs_flat_explore"] = round(e2e["update_ms"] / table["explore"]["avg_ms"], 4)
+        # the same Runner with its gradients from the gradient arena (BDL_GRAD_ARENA=1)
+        en = e2e_steps(a.e2e_steps, 3, local, 42, arena=True)
+        e2e["arena"] = {k: en[k] for k in ("ms_per_step", "update_ms", "grads_in_arena")}
         eg = e2e_steps(a.e2e_steps, 3, local, 42, graph=True)
         e2e["graph_ms_per_step"] = eg["ms_per_step"]
         e2e["graph_steps_per_s"] = eg["steps_per_s"]
+        e2e["graph_update_ms"] = eg["update_ms"]
         # the update captured in the graph, bucket by bucket beside backward
         if os.environ.get("BDL_BENCH_GRAPH_OVERLAP", "0") == "1":
             eo = e2e_steps(a.e2e_steps, 3, local, 42, graph=True, overlap=True)

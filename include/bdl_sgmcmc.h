@@ -338,7 +338,11 @@ int bdl_set_launch_config(int32_t blocks_per_cu, int32_t unroll, int32_t grid_st
  * thread's bdl_sgmcmc_step calls launch nothing; each rewrites `node`'s kernel
  * arguments in the instantiated graph (hipGraphExecKernelNodeSetParams) with
  * the step it describes, which must select the kernel the node was captured
- * with (checked first: else BDL_ERR_ARG, nothing changed).  graph_exec = null ends the redirect. */
+ * with (checked first: else BDL_ERR_ARG, nothing changed).  graph_exec = null ends the redirect.
+ * While a redirect is set, the thread's other launching entry points
+ * (bdl_sgld_step_clipped, bdl_adam_step, bdl_moments_update,
+ * bdl_posterior_sample, bdl_philox_normal, bdl_stream_mix) launch nothing and
+ * return BDL_ERR_ARG. */
 int bdl_graph_find_step_node(void* graph, const void* theta, int64_t n, void** node);
 /* The arguments a captured step node launches with (a diagnostic, read
  * before the first replay): out[0..9] = theta, grad, mom, runs, grad_base,

@@ -11,16 +11,20 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "bdl_sgmcmc.h")
-HEADERS = [HEADER, os.path.join(ROOT, "include", "bdl_measure.h")]
+HEADERS = [HEADER, os.path.join(ROOT, "include", "bdl_measure.h"),
+           os.path.join(ROOT, "include", "bdl_arena.h")]
 
 
 def declared_functions(headers=HEADERS):
     txt = "".join(open(h).read() for h in headers)
-    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(bdl_\w+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*|void\*?)\s+(bdl_\w+)\(", txt, re.M)))
 
 
 def test_header_declares_expected_api():
     assert declared_functions([HEADERS[1]]) == ["bdl_stream_mix"]
+    assert declared_functions([HEADERS[2]]) == sorted([
+        "bdl_arena_reserve", "bdl_arena_alloc", "bdl_arena_free", "bdl_arena_stats",
+        "bdl_arena_contains"])
     assert declared_functions([HEADER]) == sorted([
         "bdl_version", "bdl_last_error", "bdl_build_runs", "bdl_sgmcmc_step",
         "bdl_moments_update", "bdl_posterior_sample", "bdl_philox_normal",
@@ -209,6 +213,34 @@ def test_entry_points_validate_before_touching_the_device():
     a.mom1 = 0x9000
     assert h.bdl_adam_step(a, ad, None) == -3                       # Welford not an Adam collect
     assert b"bdl_adam_step" in h.bdl_last_error()
+
+
+def test_other_entry_points_refuse_while_a_graph_redirect_is_active():
+    """Only bdl_sgmcmc_step rewrites a captured node: while a redirect is set,
+    every other launching entry point launches nothing and says why (a
+    pointer check before any HIP call; the fake handles are never used)."""
+    from bayesdll_amd import _lib as L
+    h = L.lib()
+    assert h.bdl_graph_redirect(C.c_void_p(0x10), C.c_void_p(0x20)) == 0
+    try:
+        a, ad = L.StepArgs(), L.AdamArgs()
+        a.method, a.n = L.ADAM_SGHMC, 8
+        calls = {
+            "bdl_adam_step": lambda: h.bdl_adam_step(a, ad, None),
+            "bdl_sgld_step_clipped": lambda: h.bdl_sgld_step_clipped(a, 1.0, C.c_void_p(0x6000),
+                                                                     None),
+            "bdl_moments_update": lambda: h.bdl_moments_update(L.MomentsArgs(), None),
+            "bdl_posterior_sample": lambda: h.bdl_posterior_sample(L.SampleArgs(), None),
+            "bdl_philox_normal": lambda: h.bdl_philox_normal(C.c_void_p(0x1000), 8, 0, 0, 0, None),
+            "bdl_stream_mix": lambda: h.bdl_stream_mix((C.c_void_p * 1)(0x1000), 1,
+                                                       (C.c_void_p * 1)(0x2000), 1, 8, 1, 1, None),
+        }
+        for name, call in calls.items():
+            assert call() == -3, name
+            assert b"graph redirect is active" in h.bdl_last_error(), name
+    finally:
+        h.bdl_graph_redirect(None, None)
+    assert h.bdl_moments_update(None, None) == -1  # back to ordinary validation
 
 
 def test_plain_c_host_links_and_calls_the_abi(tmp_path):

@@ -18,7 +18,7 @@ def _need_gpu():
         pytest.skip("needs a HIP device")
 
 
-def _run(graph, overlap, monkeypatch):
+def _run(graph, overlap, monkeypatch, between=None):
     import bayesdll_amd._base as B
     import bayesdll_amd.csghmc as csghmc
     from fakenet import MLP, init_vector, synthetic_mnist
@@ -50,6 +50,8 @@ def _run(graph, overlap, monkeypatch):
                 else:
                     coll = (2, m1, m2, float(step))  # COLLECT_WELFORD
             lr = 1e-2 * (1.0 + 0.1 * step)
+            if between is not None:
+                between(step)
             loss, _ = model(x, y, net, None, crit, [lr, 2 * lr], 1.0, 0.5,
                             should_sample=k % 2 == 1, collect=coll)
             losses.append(float(loss))
@@ -70,4 +72,56 @@ def test_graph_overlap_equals_eager_chain(monkeypatch):
     assert torch.equal(mg.flat.theta, me.flat.theta)
     assert torch.equal(mg.flat.mom, me.flat.mom)
     assert torch.equal(m1g, m1e) and torch.equal(m2g, m2e)
+    mg.release_graphs()
+
+
+def _same(a, b):
+    ma, m1a, m2a, la = a
+    mb, m1b, m2b, lb = b
+    assert la == lb
+    assert torch.equal(ma.flat.theta, mb.flat.theta)
+    assert torch.equal(ma.flat.mom, mb.flat.mom)
+    assert torch.equal(m1a, m1b) and torch.equal(m2a, m2b)
+
+
+def test_failed_node_check_falls_back_once(monkeypatch):
+    """A capture whose node check fails is dropped and the sampler stays on
+    the eager overlap from then on: ONE capture attempt, not one per step."""
+    import bayesdll_amd._base as B
+    monkeypatch.setattr(B.FusedModelBase, "_check_overlap_nodes",
+                        staticmethod(lambda *a: "forced mismatch"))
+    got = _run(True, True, monkeypatch)
+    mg = got[0]
+    assert mg.overlap_graph_failed and mg.overlap_graph_error == "forced mismatch"
+    assert mg.overlap_captures == 1
+    assert not any("overlap" in k for k in mg._graphs)
+    monkeypatch.undo()
+    _same(got, _run(False, False, monkeypatch))
+    mg.release_graphs()
+
+
+def test_geometry_change_between_steps_keeps_the_graph(monkeypatch):
+    """Another launch geometry installed between steps (e.g. by another
+    sampler's state): every redirect re-installs the geometry its nodes were
+    captured with, so no rewrite fails and the chain stays bit-identical."""
+    from bayesdll_amd import kernels as K
+    geoms = [(1, 4, 1), (2, 2, 1), (3, 1, 1)]
+    got = _run(True, True, monkeypatch, between=lambda s: K.set_launch_config(*geoms[s % 3]))
+    mg = got[0]
+    assert not mg.overlap_graph_failed, mg.overlap_graph_error
+    assert mg.overlap_captures == sum(1 for k in mg._graphs if "overlap" in k)
+    _same(got, _run(False, False, monkeypatch))
+    mg.release_graphs()
+
+
+def test_graph_cap_reached_steps_run_eager_overlap(monkeypatch):
+    """Past MAX_OVERLAP_GRAPHS the remaining step kinds run the eager overlap,
+    bit-identical, without capturing more."""
+    import bayesdll_amd._base as B
+    monkeypatch.setattr(B, "MAX_OVERLAP_GRAPHS", 2)
+    got = _run(True, True, monkeypatch)
+    mg = got[0]
+    assert sum(1 for k in mg._graphs if "overlap" in k) <= 2
+    assert mg.overlap_captures <= 2 and not mg.overlap_graph_failed
+    _same(got, _run(False, False, monkeypatch))
     mg.release_graphs()
