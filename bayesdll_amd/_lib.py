@@ -21,6 +21,7 @@ BDL_OK = 0
 CSGHMC, SGHMC, SGLD, SGHMC_GRAD, SGLD_GRAD, ADAM_SGHMC, ADAM_SGHMC_GRAD = range(7)
 NOISE_NONE, NOISE_BUFFER, NOISE_PHILOX = 0, 1, 2
 COLLECT_NONE, COLLECT_WELFORD_INIT, COLLECT_WELFORD, COLLECT_MEAN_INIT, COLLECT_MEAN = range(5)
+MIX_BARE, MIX_PIPELINED, MIX_PACED = 0, 1, 2  # include/bdl_measure.h bdl_mix_schedule
 ATTR_HEAD, ATTR_PRIOR, ATTR_SKIP, ATTR_GUNALIGNED = 0x1, 0x2, 0x4, 0x8
 FLAG_FIRST_STEP, FLAG_RECIP_DIV, FLAG_MOMENTUM, FLAG_GRAD_READY = 0x1, 0x2, 0x4, 0x8
 VAR_GIVEN, VAR_RAW_MOMENTS, VAR_WELFORD = 0, 1, 2
@@ -103,6 +104,10 @@ EXPORTS = {
     # include/bdl_measure.h
     "bdl_stream_mix": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.POINTER(C.c_void_p),
                                  C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_void_p]),
+    "bdl_sgmcmc_step_bare": (C.c_int, [C.POINTER(StepArgs), C.c_void_p]),
+    "bdl_stream_mix_schedule": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32,
+                                          C.POINTER(C.c_void_p), C.c_int32, C.c_int64,
+                                          C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
     # include/bdl_arena.h
     "bdl_arena_reserve": (C.c_int, [C.c_int32, C.c_int64]),
     "bdl_arena_alloc": (C.c_void_p, [C.c_size_t, C.c_int, C.c_void_p]),

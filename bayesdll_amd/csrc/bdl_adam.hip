@@ -10,6 +10,11 @@ StepKernel pick_adam_unroll(int unroll) {
   if constexpr (NOISE == BDL_NOISE_NONE) {
     (void)unroll;
     return bdl_adam_kernel<NOISE, COLLECT, false, 2>;
+  } else if constexpr (NOISE == BDL_NOISE_BUFFER && COLLECT != BDL_COLLECT_NONE) {
+    // the buffer-noise collect at depth 4 holds eleven streams in two
+    // register sets and spilled VGPRs to scratch (164-188 B/lane): depth <= 2
+    return unroll == 1 ? bdl_adam_kernel<NOISE, COLLECT, false, 1>
+                       : bdl_adam_kernel<NOISE, COLLECT, false, 2>;
   } else {
     switch (unroll) {
       case 1:

@@ -556,7 +556,7 @@ int no_redirect(const char* what) {
               "only bdl_sgmcmc_step rewrites a node");
 }
 
-int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
+int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream, bool bare = false) {
   if (!s) return fail(BDL_ERR_NULL, "bdl_sgmcmc_step: null args");
   if (s->n < 0) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: n < 0");
   if (s->method < BDL_CSGHMC || s->method > BDL_SGLD_GRAD)
@@ -587,7 +587,9 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
     if (p && !aligned16(p)) return fail(BDL_ERR_ALIGN, "bdl_sgmcmc_step: vector not 16-B aligned");
 
   const int unroll = g_unroll;
-  StepKernel k = pick_step(s->method, s->noise_mode, s->collect, unroll);
+  StepKernel k = bare ? (s->method == BDL_CSGHMC ? pick_step_csghmc_bare(s->collect, unroll)
+                                                 : nullptr)
+                      : pick_step(s->method, s->noise_mode, s->collect, unroll);
   if (!k) return fail(BDL_ERR_ARG, "bdl_sgmcmc_step: unsupported method/noise/collect combination");
 
   const int64_t ngroups = (s->n + 3) / 4;
@@ -683,12 +685,21 @@ int launch_step(const bdl_step_args* s, const float* clip, hipStream_t stream) {
 
 
 // ---------------------------------------------------------------------------
-// Bare access mix of a sweep (measurement only, bdl_stream_mix): NR 16-B
-// streams read and NW written per float4 group with no arithmetic beyond a
-// sum, in the step kernels' loop shape (unguarded full iterations with all
-// loads first, one guarded tail iteration) — the HBM ceiling of a kernel's
-// exact access pattern on its exact buffers.  Written values: r0 + 0 * r1 +
-// ... (finite, usually r0).
+// Bare access mix of a sweep (measurement only, bdl_stream_mix /
+// bdl_stream_mix_schedule): NR 16-B streams read and NW written per float4
+// group with no arithmetic beyond a sum, in the step kernels' loop shape
+// (unguarded full iterations, one guarded tail iteration) — the HBM ceiling
+// of a kernel's exact access pattern on its exact buffers.  Written values:
+// r0 + 0 * r1 + ... (finite, usually r0).  Three issue schedules, since the
+// memory system does not serve every order of the same bytes equally fast
+// and a ceiling is the fastest of them:
+//   BARE       every load of an iteration, then every store;
+//   PIPELINED  the next iteration's loads issued before this one's stores
+//              (two register sets, as the Adam sweep);
+//   PACED      BARE with one Philox4x32-10 + Box-Muller draw per group
+//              between the loads and the stores (the noise-bearing sweeps'
+//              arithmetic, multiplied by 0 into the written value): the
+//              spacing of a real sweep's stores without its update.
 // ---------------------------------------------------------------------------
 constexpr int kMixMaxR = 8, kMixMaxW = 6;
 struct MixArgs {
@@ -697,28 +708,56 @@ struct MixArgs {
   int64_t n;
 };
 
-template <int NR, int NW, int U>
+template <int NR, int U>
+__device__ __forceinline__ void mix_load(const MixArgs& a, int64_t gb, f4v (&x)[U][NR]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) x[u][r] = vload(a.r[r] + e);
+  }
+}
+
+template <int NR, int NW, int U, bool PACED>
+__device__ __forceinline__ void mix_store(const MixArgs& a, int64_t gb, f4v (&x)[U][NR]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    const int64_t e = gi * 4;
+    f4v acc = x[u][0];
+#pragma unroll
+    for (int r = 1; r < NR; ++r) acc = acc + x[u][r] * 0.0f;
+    if constexpr (PACED) acc = acc + philox_normal4((uint64_t)gi, 0x5eedull, 0, 1) * 0.0f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) vstore(a.w[w] + e, acc);
+  }
+}
+
+template <int NR, int NW, int U, int S>
 __global__ __launch_bounds__(kBlock) void bdl_mix_kernel(const MixArgs a) {
   constexpr int64_t kIter = (int64_t)kBlock * U;
   const int64_t ngroups = (a.n + 3) >> 2, nfull = a.n >> 2;
   const int64_t stride = (int64_t)gridDim.x * kIter;
   int64_t gb = (int64_t)blockIdx.x * kIter;
-  for (; gb + kIter <= nfull; gb += stride) {
-    f4v x[U][NR];
+  if constexpr (S == BDL_MIX_PIPELINED) {
+    f4v x[U][NR], y[U][NR];
+    if (gb + kIter <= nfull) mix_load<NR, U>(a, gb, x);
+    for (; gb + kIter <= nfull; gb += stride) {
+      const bool more = gb + stride + kIter <= nfull;
+      if (more) mix_load<NR, U>(a, gb + stride, y);
+      mix_store<NR, NW, U, false>(a, gb, x);
+      if (more) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+        for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int r = 0; r < NR; ++r) x[u][r] = vload(a.r[r] + e);
+          for (int r = 0; r < NR; ++r) x[u][r] = y[u][r];
+      }
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
-      f4v acc = x[u][0];
-#pragma unroll
-      for (int r = 1; r < NR; ++r) acc = acc + x[u][r] * 0.0f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) vstore(a.w[w] + e, acc);
+  } else {
+    for (; gb + kIter <= nfull; gb += stride) {
+      f4v x[U][NR];
+      mix_load<NR, U>(a, gb, x);
+      mix_store<NR, NW, U, S == BDL_MIX_PACED>(a, gb, x);
     }
   }
   if (gb < ngroups) {
@@ -735,24 +774,34 @@ __global__ __launch_bounds__(kBlock) void bdl_mix_kernel(const MixArgs a) {
 
 typedef void (*MixKernel)(const MixArgs);
 
-template <int NR, int NW>
+template <int NR, int NW, int S>
 MixKernel pick_mix_u(int unroll) {
   switch (unroll) {
-    case 1: return bdl_mix_kernel<NR, NW, 1>;
-    case 4: return bdl_mix_kernel<NR, NW, 4>;
-    default: return bdl_mix_kernel<NR, NW, 2>;
+    case 1: return bdl_mix_kernel<NR, NW, 1, S>;
+    case 4: return bdl_mix_kernel<NR, NW, 4, S>;
+    default: return bdl_mix_kernel<NR, NW, 2, S>;
   }
+}
+
+template <int NR, int NW>
+MixKernel pick_mix_s(int schedule, int unroll) {
+  switch (schedule) {
+    case BDL_MIX_BARE: return pick_mix_u<NR, NW, BDL_MIX_BARE>(unroll);
+    case BDL_MIX_PIPELINED: return pick_mix_u<NR, NW, BDL_MIX_PIPELINED>(unroll);
+    case BDL_MIX_PACED: return pick_mix_u<NR, NW, BDL_MIX_PACED>(unroll);
+  }
+  return nullptr;
 }
 
 // the mixes of the path's sweeps: draw (2, 1), explore / moments (3, 2),
 // SGLD (4, 2), Welford init (3, 4), Welford collect (5, 4), Adam + SGD (7, 5)
-MixKernel pick_mix(int nr, int nw, int unroll) {
-  if (nr == 2 && nw == 1) return pick_mix_u<2, 1>(unroll);
-  if (nr == 3 && nw == 2) return pick_mix_u<3, 2>(unroll);
-  if (nr == 4 && nw == 2) return pick_mix_u<4, 2>(unroll);
-  if (nr == 3 && nw == 4) return pick_mix_u<3, 4>(unroll);
-  if (nr == 5 && nw == 4) return pick_mix_u<5, 4>(unroll);
-  if (nr == 7 && nw == 5) return pick_mix_u<7, 5>(unroll);
+MixKernel pick_mix(int nr, int nw, int schedule, int unroll) {
+  if (nr == 2 && nw == 1) return pick_mix_s<2, 1>(schedule, unroll);
+  if (nr == 3 && nw == 2) return pick_mix_s<3, 2>(schedule, unroll);
+  if (nr == 4 && nw == 2) return pick_mix_s<4, 2>(schedule, unroll);
+  if (nr == 3 && nw == 4) return pick_mix_s<3, 4>(schedule, unroll);
+  if (nr == 5 && nw == 4) return pick_mix_s<5, 4>(schedule, unroll);
+  if (nr == 7 && nw == 5) return pick_mix_s<7, 5>(schedule, unroll);
   return nullptr;
 }
 
@@ -894,6 +943,13 @@ int bdl_build_runs(const bdl_segment* segs, int32_t nseg, int64_t n, bdl_run* ou
 
 int bdl_sgmcmc_step(const bdl_step_args* s, void* stream) {
   return launch_step(s, nullptr, (hipStream_t)stream);
+}
+
+int bdl_sgmcmc_step_bare(const bdl_step_args* s, void* stream) {
+  if (const int rc = no_redirect("bdl_sgmcmc_step_bare")) return rc;
+  if (s && s->method != BDL_CSGHMC)
+    return fail(BDL_ERR_ARG, "bdl_sgmcmc_step_bare: the bare sweep exists for cSGHMC only");
+  return launch_step(s, nullptr, (hipStream_t)stream, true);
 }
 
 int64_t bdl_clip_workspace_bytes(int64_t n) {
@@ -1124,15 +1180,18 @@ int bdl_posterior_sample(const bdl_sample_args* s, void* stream) {
   return BDL_OK;
 }
 
-int bdl_stream_mix(const float* const* reads, int32_t nreads, float* const* writes,
-                   int32_t nwrites, int64_t n, int32_t blocks_per_cu, int32_t unroll,
-                   void* stream) {
+int bdl_stream_mix_schedule(const float* const* reads, int32_t nreads, float* const* writes,
+                            int32_t nwrites, int64_t n, int32_t blocks_per_cu, int32_t unroll,
+                            int32_t schedule, void* stream) {
   if (const int rc = no_redirect("bdl_stream_mix")) return rc;
   if (!reads || !writes) return fail(BDL_ERR_NULL, "bdl_stream_mix: null stream list");
   if (n < 0 || blocks_per_cu < 1 || blocks_per_cu > 16)
     return fail(BDL_ERR_ARG, "bdl_stream_mix: n >= 0 and blocks_per_cu in [1, 16]");
-  MixKernel k = (nreads <= kMixMaxR && nwrites <= kMixMaxW) ? pick_mix(nreads, nwrites, unroll)
-                                                            : nullptr;
+  if (schedule < BDL_MIX_BARE || schedule > BDL_MIX_PACED)
+    return fail(BDL_ERR_ARG, "bdl_stream_mix: schedule is BDL_MIX_BARE, _PIPELINED or _PACED");
+  MixKernel k = (nreads <= kMixMaxR && nwrites <= kMixMaxW)
+                    ? pick_mix(nreads, nwrites, schedule, unroll)
+                    : nullptr;
   if (!k)
     return fail(BDL_ERR_ARG, "bdl_stream_mix: supported (reads, writes): (2,1) (3,2) (4,2) "
                 "(3,4) (5,4) (7,5)");
@@ -1160,6 +1219,13 @@ int bdl_stream_mix(const float* const* reads, int32_t nreads, float* const* writ
     return BDL_ERR_LAUNCH;
   }
   return BDL_OK;
+}
+
+int bdl_stream_mix(const float* const* reads, int32_t nreads, float* const* writes,
+                   int32_t nwrites, int64_t n, int32_t blocks_per_cu, int32_t unroll,
+                   void* stream) {
+  return bdl_stream_mix_schedule(reads, nreads, writes, nwrites, n, blocks_per_cu, unroll,
+                                 BDL_MIX_BARE, stream);
 }
 
 int bdl_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t chain, uint64_t step,

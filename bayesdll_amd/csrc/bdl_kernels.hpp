@@ -184,12 +184,28 @@ struct KArgs {
   float inv_s2, inv_nd, inv_ca, inv_cb, inv_temp, inv_bc1, inv_bc2;
 };
 
+// The kernel's KArgs re-read from the kernarg segment at the point of use:
+// scalar loads behind a laundered segment pointer, which the compiler can
+// neither hoist out of the sweep loop nor keep in SGPRs across it.  Every
+// step / Adam kernel takes its KArgs as the first kernel argument, at offset
+// 0 of the segment.  The sweep's device functions are templates over the
+// argument view A (KArgs, or this address-space-4 view), so one body serves
+// both.
+typedef __attribute__((address_space(4))) const KArgs ckargs;
+
+__device__ __forceinline__ ckargs& fresh_kargs() {
+  ckargs* ap = (ckargs*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(ap));
+  return *ap;
+}
+
 // The Philox draw for float4 group gi of a launch.  The counter is the group
 // index within its chain: with stacked chains (cgroups > 0, chain k's elements
 // at [4*cgroups*k, 4*cgroups*(k+1))) chain k is keyed chain + k and draws what
 // a one-chain launch with that chain id draws.  The host keeps every group
 // index below 2^32 in that mode, so the split is a 32-bit division.
-__device__ __forceinline__ f4v step_noise4(const KArgs& a0, int64_t gi) {
+template <class A>
+__device__ __forceinline__ f4v step_noise4(const A& a0, int64_t gi) {
 #ifdef BDL_PHILOX_KEYS_PER_CALL
   // the generator's inputs (seed, chain, step, offset, chain split) re-read
   // from the kernarg segment per call (scalar loads) instead of being held in
@@ -202,7 +218,7 @@ __device__ __forceinline__ f4v step_noise4(const KArgs& a0, int64_t gi) {
   asm volatile("" : "+s"(ap));
   ckargs& a = *ap;
 #else
-  const KArgs& a = a0;
+  const A& a = a0;
 #endif
   uint64_t g = (uint64_t)gi + a.goff, c = a.chain;
   if (a.cgroups) {
@@ -258,7 +274,8 @@ __device__ __forceinline__ void stage_runs(const KArgs& a) {
 }
 
 // Where run r's gradient lives: the flat vector, or its own tensor.
-__device__ __forceinline__ float* run_grad(const KArgs& a, int r) {
+template <class A>
+__device__ __forceinline__ float* run_grad(const A& a, int r) {
   return a.gbase ? reinterpret_cast<float*>(lds_gbase(a.nruns)[r]) : a.grad;
 }
 
@@ -291,6 +308,33 @@ __device__ __forceinline__ int find_run_lds(int nruns, int64_t idx) {
   return lo;
 }
 
+// The cSGHMC sweep with its arithmetic removed (measurement only,
+// bdl_sgmcmc_step_bare): the same loop, run table, loads and stores as the
+// production cSGHMC kernel of a collect kind, the update and the noise draw
+// gone (theta, mom, m1, m2 written back as loaded; the init kinds' m1 = theta,
+// m2 = 0 / theta^2 kept: they are copies).  Its time is the ceiling of that
+// kernel's own access schedule.  Not a public method id.
+constexpr int kMethodBare = 100;
+
+template <int METHOD>
+constexpr bool is_csghmc_sweep() {
+  return METHOD == BDL_CSGHMC || METHOD == kMethodBare;
+}
+
+// the collect arithmetic a METHOD applies: for the bare sweep's steady-state
+// kinds none — m1 / m2 go back as loaded, laundered through an empty asm so
+// that the compiler keeps the load and the store (a store of the value just
+// loaded from the same address is otherwise deleted as dead)
+constexpr int kCollectLaunder = 99;
+
+template <int METHOD, int COLLECT>
+constexpr int collect_op() {
+  return (METHOD == kMethodBare &&
+          (COLLECT == BDL_COLLECT_WELFORD || COLLECT == BDL_COLLECT_MEAN))
+             ? kCollectLaunder
+             : COLLECT;
+}
+
 struct StepConst {
   bool sgd_mom, sgd_mom_read, has_m2, grad_ready, clip;
   float inv_s2, inv_nd, inv_ca, inv_cb, clip_coef;
@@ -302,11 +346,15 @@ struct StepConst {
 // eta / ns are the element's lr and noise scale (its lr group), PRIOR whether
 // the Gaussian-prior term applies, GR = grad already formed (SGD step only).
 // ---------------------------------------------------------------------------
-template <int METHOD, int NOISE, bool RECIP, bool PRIOR, bool GR>
-__device__ __forceinline__ void update_core(const KArgs& a, const StepConst& c, float eta,
+template <int METHOD, int NOISE, bool RECIP, bool PRIOR, bool GR, class A>
+__device__ __forceinline__ void update_core(const A& a, const StepConst& c, float eta,
                                             float ns, float& th, float& g, float& v, float th0,
                                             float eps) {
-  if constexpr (GR) {
+  if constexpr (METHOD == kMethodBare) {
+    // loaded values go back unchanged, through an empty asm (collect_op)
+    (void)a, (void)c, (void)eta, (void)ns, (void)th0, (void)eps;
+    asm volatile("" : "+v"(th), "+v"(g), "+v"(v));
+  } else if constexpr (GR) {
     // the sampler gradient was formed (and possibly clipped) by a previous
     // *_GRAD launch: only torch.optim.SGD's step remains
     float stepv = g;
@@ -369,7 +417,10 @@ __device__ __forceinline__ void update_core(const KArgs& a, const StepConst& c, 
 template <int COLLECT, bool RECIP, class A>
 __device__ __forceinline__ void collect_core(const A& a, const StepConst& c, float th,
                                              float& m1, float& m2) {
-  if constexpr (COLLECT == BDL_COLLECT_WELFORD_INIT) {
+  if constexpr (COLLECT == kCollectLaunder) {
+    (void)a, (void)c, (void)th;
+    asm volatile("" : "+v"(m1), "+v"(m2));
+  } else if constexpr (COLLECT == BDL_COLLECT_WELFORD_INIT) {
     m1 = th;
     m2 = 0.0f;
   } else if constexpr (COLLECT == BDL_COLLECT_WELFORD) {
@@ -389,22 +440,43 @@ __device__ __forceinline__ void collect_core(const A& a, const StepConst& c, flo
 // Per-kernel constants of a method / collect combination.
 template <int METHOD, int COLLECT>
 struct StepTraits {
-  static constexpr bool kReadPrior = (METHOD != BDL_CSGHMC);
-  static constexpr bool kMom =
-      (METHOD == BDL_CSGHMC || METHOD == BDL_SGHMC || METHOD == BDL_SGHMC_GRAD);
+  static constexpr bool kReadPrior = !is_csghmc_sweep<METHOD>();
+  static constexpr bool kMom = (is_csghmc_sweep<METHOD>() || METHOD == BDL_SGHMC ||
+                                METHOD == BDL_SGHMC_GRAD);
   static constexpr bool kWriteTheta =
-      (METHOD == BDL_CSGHMC || METHOD == BDL_SGHMC || METHOD == BDL_SGLD);
+      (is_csghmc_sweep<METHOD>() || METHOD == BDL_SGHMC || METHOD == BDL_SGLD);
   static constexpr bool kWriteGrad = (METHOD == BDL_SGHMC_GRAD || METHOD == BDL_SGLD_GRAD);
   static constexpr bool kCollect = (COLLECT != BDL_COLLECT_NONE);
   static constexpr bool kReadMoments =
       (COLLECT == BDL_COLLECT_WELFORD || COLLECT == BDL_COLLECT_MEAN);
 };
 
+// Is A the re-read kernarg view (fresh_kargs) rather than the kernel's KArgs?
+template <class A>
+constexpr bool is_fresh_args = !__is_same(__remove_cv(A), KArgs);
+
+// Which step instances run their sweep on the re-read argument view (stream
+// bases, scalars and flags loaded per iteration) with the slow path rolled:
+// the SGLD / SGHMC collect and buffer-noise instances at depth 2 and 4.
+// Those spilled 2-16 SGPRs, and the reloads sat in the sweep loop (16-42
+// v_readlane per loop; 0 with this, tools/hot_loop_spills.py).  Same
+// process, builds alternating (profiles/round6/ab_spills/): ResNet-101 SGLD
+// collect 0.3079 ms (1 x 4) vs 0.3102 (best, 2 x 1), SGHMC collect 0.2970 vs
+// 0.3026 at 1 x 2, ViT-L/32 SGLD collect equal.  At depth 1 the per-iteration
+// scalar loads cost 5-21 % (the wave waits on them once per group), so the
+// depth-1 instances keep SGPR-resident arguments, as do the cSGHMC sweeps
+// (0 spills in every Philox instance).
+template <int METHOD, int NOISE, int COLLECT, int UNROLL>
+constexpr bool fresh_step_args() {
+  return !is_csghmc_sweep<METHOD>() && UNROLL >= 2 &&
+         (COLLECT != BDL_COLLECT_NONE || NOISE == BDL_NOISE_BUFFER);
+}
+
 // FAST PATH: a whole block-iteration (kBlock*UNROLL float4 groups) in range
 // and inside one non-skip run.  eta / ns are scalars, PRIOR / GR compile-time:
 // no branch inside, no bounds checks, every load issued before any arithmetic.
-template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL, bool PRIOR, bool GR>
-__device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, int64_t gb,
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL, bool PRIOR, bool GR, class A>
+__device__ __forceinline__ void chunk_fast(const A& a, const StepConst& c, int64_t gb,
                                            float eta, float ns, float* gp, uint32_t& bad) {
   using T = StepTraits<METHOD, COLLECT>;
   constexpr bool kPriorLoad = T::kReadPrior && PRIOR && !GR;
@@ -449,7 +521,7 @@ __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, i
     for (int j = 0; j < 4; ++j) {
       float xt = th[u][j], xg = g[u][j], xv = v[u][j], x1 = m1[u][j], x2 = m2[u][j];
       update_core<METHOD, NOISE, RECIP, PRIOR, GR>(a, c, eta, ns, xt, xg, xv, t0[u][j], ep[u][j]);
-      collect_core<COLLECT, RECIP>(a, c, xt, x1, x2);
+      collect_core<collect_op<METHOD, COLLECT>(), RECIP>(a, c, xt, x1, x2);
       th[u][j] = xt;
       g[u][j] = xg;
       v[u][j] = xv;
@@ -475,14 +547,14 @@ __device__ __forceinline__ void chunk_fast(const KArgs& a, const StepConst& c, i
   }
 }
 
-template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
-__device__ __forceinline__ void chunk_fast_dispatch(const KArgs& a, const StepConst& c,
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL, class A>
+__device__ __forceinline__ void chunk_fast_dispatch(const A& a, const StepConst& c,
                                                     int64_t gb, uint32_t attr, float* gp,
                                                     uint32_t& bad) {
   const bool head = (attr & BDL_ATTR_HEAD) != 0;
   const float eta = head ? a.lr1 : a.lr0;
   const float ns = head ? a.ns1 : a.ns0;
-  if constexpr (METHOD == BDL_CSGHMC) {
+  if constexpr (is_csghmc_sweep<METHOD>()) {
     chunk_fast<METHOD, NOISE, COLLECT, RECIP, UNROLL, false, false>(a, c, gb, eta, ns, gp, bad);
   } else {
     if constexpr (METHOD == BDL_SGLD || METHOD == BDL_SGHMC) {
@@ -515,8 +587,8 @@ __device__ __forceinline__ int64_t fast_run(const KArgs& a, const StepConst& c, 
 }
 
 // Element-wise update for the slow path: attribute-dependent branches allowed.
-template <int METHOD, int NOISE, int COLLECT, bool RECIP>
-__device__ __forceinline__ void update_elem(const KArgs& a, const StepConst& c, uint32_t attr,
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, class A>
+__device__ __forceinline__ void update_elem(const A& a, const StepConst& c, uint32_t attr,
                                             float& th, float& g, float& v, float th0, float eps,
                                             float& m1, float& m2) {
   const bool head = (attr & BDL_ATTR_HEAD) != 0;
@@ -532,20 +604,23 @@ __device__ __forceinline__ void update_elem(const KArgs& a, const StepConst& c, 
       update_core<METHOD, NOISE, RECIP, false, false>(a, c, eta, ns, th, g, v, th0, eps);
     }
   }
-  collect_core<COLLECT, RECIP>(a, c, th, m1, m2);
+  collect_core<collect_op<METHOD, COLLECT>(), RECIP>(a, c, th, m1, m2);
 }
 
 // SLOW PATH: an iteration that reaches the end of the vector / span, crosses a
 // run boundary or covers a skipped parameter.  Per-lane predicates, guarded
 // partial groups, a per-element run search (in LDS).  Taken for
 // O(#runs + #blocks) iterations per launch.
-template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
-__device__ __forceinline__ void chunk_slow(const KArgs& a, const StepConst& c, int64_t gb,
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL, class A>
+__device__ __forceinline__ void chunk_slow(const A& a, const StepConst& c, int64_t gb,
                                            int64_t gend, int r0, uint32_t& bad) {
   using T = StepTraits<METHOD, COLLECT>;
   const int64_t n = a.n;
   int rr = r0;  // run of the chunk's first element; a lane's elements only move forward
-#pragma unroll
+  // rolled in the fresh-argument instances (fresh_step_args): the path is
+  // rare, and unrolled, its nested guards' lane masks filled their SGPR file
+  constexpr int kSlowUnroll = is_fresh_args<A> ? 1 : UNROLL;
+#pragma unroll kSlowUnroll
   for (int u = 0; u < UNROLL; ++u) {
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
     if (gi >= gend) continue;
@@ -628,8 +703,8 @@ __device__ __forceinline__ bool multi_run_ok(int nruns, int r, int64_t e_end) {
 // when each tensor's gradient is read from its own autograd allocation (one
 // run per tensor: ~300 of the ~75 K iterations of a ViT-L/32 step), which
 // the guarded slow path used to take with its loads serialised per group.
-template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL>
-__device__ __forceinline__ void chunk_multi(const KArgs& a, const StepConst& c, int64_t gb,
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL, class A>
+__device__ __forceinline__ void chunk_multi(const A& a, const StepConst& c, int64_t gb,
                                             int r0, uint32_t& bad) {
   using T = StepTraits<METHOD, COLLECT>;
   f4v th[UNROLL], g[UNROLL], v[UNROLL], t0[UNROLL], ep[UNROLL], m1[UNROLL], m2[UNROLL];
@@ -686,13 +761,159 @@ __device__ __forceinline__ void chunk_multi(const KArgs& a, const StepConst& c, 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Software-pipelined cSGHMC collect sweep (sample steps that update the
+// posterior moments: Welford init, Welford, running-mean collects): the next
+// block iteration's loads are issued before this iteration's Philox draw,
+// update and stores, so at one wave per SIMD — the geometry the collects
+// tune to — the draw no longer sits between a load's return and the next
+// load's issue.  Two register sets take turns (the loop body written twice
+// with the roles swapped); an iteration that needs the multi-run or guarded
+// path drains the pipeline.  Same per-element update as chunk_fast (PRIOR and
+// GR never apply to cSGHMC), so results are bit-identical.
+// ---------------------------------------------------------------------------
+template <int COLLECT>
+constexpr bool pipe_csghmc_collect() {
+#ifdef BDL_PIPE_CSGHMC_COLLECT
+  return COLLECT != BDL_COLLECT_NONE;
+#else
+  return false;
+#endif
+}
+
+template <int U>
+struct CsgRegs {
+  f4v th[U], g[U], v[U], m1[U], m2[U];
+};
+
+template <int COLLECT, int U>
+__device__ __forceinline__ void csg_pipe_load(const KArgs& a, const StepConst& c, int64_t gb,
+                                              const float* gp, CsgRegs<U>& R) {
+  constexpr bool kReadMoments = COLLECT == BDL_COLLECT_WELFORD || COLLECT == BDL_COLLECT_MEAN;
+  const f4v z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
+    R.th[u] = vload(a.theta + e);
+    R.g[u] = vload(gp + e);
+    R.v[u] = vload(a.mom + e);
+    R.m1[u] = R.m2[u] = z;
+    if constexpr (kReadMoments) {
+      R.m1[u] = vload(a.mom1 + e);
+      if (c.has_m2) R.m2[u] = vload(a.mom2 + e);
+    }
+  }
+}
+
+template <int NOISE, int COLLECT, bool RECIP, int U>
+__device__ __forceinline__ void csg_pipe_compute(const KArgs& a, const StepConst& c, int64_t gb,
+                                                 float eta, float ns, CsgRegs<U>& R,
+                                                 uint32_t& bad) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
+    const int64_t e = gi * 4;
+    f4v ep = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (NOISE == BDL_NOISE_PHILOX) ep = step_noise4(a, gi);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float xt = R.th[u][j], xg = R.g[u][j], xv = R.v[u][j], x1 = R.m1[u][j], x2 = R.m2[u][j];
+      update_core<BDL_CSGHMC, NOISE, RECIP, false, false>(a, c, eta, ns, xt, xg, xv, 0.f, ep[j]);
+      collect_core<COLLECT, RECIP>(a, c, xt, x1, x2);
+      R.th[u][j] = xt;
+      R.v[u][j] = xv;
+      R.m1[u][j] = x1;
+      R.m2[u][j] = x2;
+    }
+    bad |= nonfinite4(R.th[u]);
+    vstore(a.theta + e, R.th[u]);
+    vstore(a.mom + e, R.v[u]);
+    vstore(a.mom1 + e, R.m1[u]);
+    if (c.has_m2) vstore(a.mom2 + e, R.m2[u]);
+  }
+}
+
+// Cursor of the pipelined sweep: the block iteration, its run, whether it
+// takes the fast path and whether its data already sit in the current set.
+struct CsgCursor {
+  int64_t gb;
+  int r;
+  uint32_t attr;
+  bool fast, loaded;
+};
+
+template <int U>
+__device__ __forceinline__ bool csg_pipe_fast(const KArgs& a, int64_t gb, int64_t g1, int& r,
+                                              uint32_t& attr) {
+  constexpr int64_t kIter = (int64_t)kBlock * U;
+  if (gb >= g1) return false;
+  while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
+  attr = run_attr(r);
+  const int64_t gend = gb + kIter;
+  return gend <= g1 && gend <= (a.n >> 2) && run_end(r) >= gend * 4 && !(attr & kNoFastPath);
+}
+
+// One block iteration with X as the current register set and Y as the next;
+// false when the block's span is done.
+template <int NOISE, int COLLECT, bool RECIP, int U>
+__device__ __forceinline__ bool csg_pipe_iter(const KArgs& a, const StepConst& c, int64_t g1,
+                                              int64_t gstep, CsgCursor& k, CsgRegs<U>& X,
+                                              CsgRegs<U>& Y, uint32_t& bad) {
+  constexpr int64_t kIter = (int64_t)kBlock * U;
+  if (k.gb >= g1) return false;
+  if (!k.fast) {
+    const int64_t gend = min(k.gb + kIter, g1);
+    if (gend == k.gb + kIter && gend <= (a.n >> 2) && multi_run_ok(a.nruns, k.r, gend * 4))
+      chunk_multi<BDL_CSGHMC, NOISE, COLLECT, RECIP, U>(a, c, k.gb, k.r, bad);
+    else
+      chunk_slow<BDL_CSGHMC, NOISE, COLLECT, RECIP, U>(a, c, k.gb, gend, k.r, bad);
+    k.gb += gstep;
+    k.fast = csg_pipe_fast<U>(a, k.gb, g1, k.r, k.attr);
+    k.loaded = false;
+    return true;
+  }
+  if (!k.loaded) csg_pipe_load<COLLECT, U>(a, c, k.gb, run_grad(a, k.r), X);
+  // the next iteration: classify it and issue its loads before this one's math
+  const int64_t nx = k.gb + gstep;
+  int rn = k.r;
+  uint32_t attrn = 0;
+  const bool fastn = csg_pipe_fast<U>(a, nx, g1, rn, attrn);
+  if (fastn) csg_pipe_load<COLLECT, U>(a, c, nx, run_grad(a, rn), Y);
+  const bool head = (k.attr & BDL_ATTR_HEAD) != 0;
+  csg_pipe_compute<NOISE, COLLECT, RECIP, U>(a, c, k.gb, head ? a.lr1 : a.lr0,
+                                             head ? a.ns1 : a.ns0, X, bad);
+  k.gb = nx;
+  k.r = rn;
+  k.attr = attrn;
+  k.fast = fastn;
+  k.loaded = fastn;
+  return true;
+}
+
+template <int NOISE, int COLLECT, bool RECIP, int U>
+__device__ __forceinline__ void csg_pipe_sweep(const KArgs& a, const StepConst& c, int64_t g0,
+                                               int64_t g1, int64_t gstep, int r, uint32_t& bad) {
+  CsgCursor k;
+  k.gb = g0;
+  k.r = r;
+  k.attr = 0;
+  k.fast = csg_pipe_fast<U>(a, k.gb, g1, k.r, k.attr);
+  k.loaded = false;
+  CsgRegs<U> A, B;
+  for (;;) {
+    if (!csg_pipe_iter<NOISE, COLLECT, RECIP, U>(a, c, g1, gstep, k, A, B, bad)) break;
+    if (!csg_pipe_iter<NOISE, COLLECT, RECIP, U>(a, c, g1, gstep, k, B, A, bad)) break;
+  }
+}
+
 // Variants of a step body, fixed per launch (step_variant): the SGD step on
 // an already formed gradient (BDL_FLAG_GRAD_READY) and the clipped SGLD
 // gradient (bdl_sgld_step_clipped); kVarRuntime reads both from the launch.
 constexpr int kVarGradReady = 1, kVarClip = 2, kVarRuntime = -1;
 
-template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL, int VAR>
-__device__ __forceinline__ void step_body(const KArgs& a) {
+// The launch's per-step constants (flags, clip coefficient, reciprocals).
+template <int METHOD, int COLLECT, int VAR, class A>
+__device__ __forceinline__ StepConst make_step_const(const A& a) {
   StepConst c;
   c.sgd_mom = (METHOD == BDL_SGLD) && (a.flags & BDL_FLAG_MOMENTUM);
   c.sgd_mom_read = c.sgd_mom && !(a.flags & BDL_FLAG_FIRST_STEP);
@@ -709,6 +930,12 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
   c.inv_nd = a.inv_nd;
   c.inv_ca = a.inv_ca;
   c.inv_cb = a.inv_cb;
+  return c;
+}
+
+template <int METHOD, int NOISE, int COLLECT, bool RECIP, int UNROLL, int VAR>
+__device__ __forceinline__ void step_body(const KArgs& a) {
+  const StepConst c = make_step_const<METHOD, COLLECT, VAR>(a);
 
   const int64_t ngroups = (a.n + 3) >> 2;
   const int64_t nfull = a.n >> 2;  // groups entirely inside [0, n)
@@ -742,7 +969,27 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
   // per-iteration run lookup, which needs fewer registers (with the per-run
   // loop: SGLD SGPR spills 0 -> 2-14 and ResNet-101 SGLD at 2 x 1 0.1793 vs
   // 0.1716 ms; cSGHMC depth-4 collects 0 -> 2-6 spills).
-  if constexpr (METHOD != BDL_CSGHMC || COLLECT != BDL_COLLECT_NONE) {
+  if constexpr (METHOD == BDL_CSGHMC && NOISE != BDL_NOISE_BUFFER &&
+                pipe_csghmc_collect<COLLECT>()) {
+    csg_pipe_sweep<NOISE, COLLECT, RECIP, UNROLL>(a, c, g0, g1, gstep, r, bad);
+  } else if constexpr (fresh_step_args<METHOD, NOISE, COLLECT, UNROLL>()) {
+  for (int64_t gb = g0; gb < g1; gb += gstep) {
+    // the iteration's arguments, flags included, from the re-read view
+    ckargs& fa = fresh_kargs();
+    const StepConst fc = make_step_const<METHOD, COLLECT, VAR>(fa);
+    while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
+    const int64_t gend = min(gb + kIter, g1);
+    const uint32_t attr = run_attr(r);
+    const bool full = gend == gb + kIter && gend <= nfull;
+    if (full && run_end(r) >= gend * 4 && !(attr & kNoFastPath))
+      chunk_fast_dispatch<METHOD, NOISE, COLLECT, RECIP, UNROLL>(fa, fc, gb, attr, run_grad(fa, r),
+                                                                  bad);
+    else if (full && multi_run_ok(a.nruns, r, gend * 4))
+      chunk_multi<METHOD, NOISE, COLLECT, RECIP, UNROLL>(fa, fc, gb, r, bad);
+    else
+      chunk_slow<METHOD, NOISE, COLLECT, RECIP, UNROLL>(fa, fc, gb, gend, r, bad);
+  }
+  } else if constexpr (!is_csghmc_sweep<METHOD>() || COLLECT != BDL_COLLECT_NONE) {
   for (int64_t gb = g0; gb < g1; gb += gstep) {
     while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
     const int64_t gend = min(gb + kIter, g1);
@@ -881,21 +1128,33 @@ __device__ __forceinline__ void adam_fast(const KArgs& a, const AdamConst& c, in
       if (c.has_m2) m2[u] = vload(a.mom2 + e);
     }
   }
+  // the update's scalars re-read from the kernarg segment (as in
+  // adam_pipe_compute): held across the sweep they spilled 89-132 SGPRs in
+  // the plain-loop (GRADONLY) instances, 12-30 this way
+  ckargs& ka = fresh_kargs();
+  AdamConst c2 = c;
+  c2.inv_s2 = ka.inv_s2;
+  c2.inv_nd = ka.inv_nd;
+  c2.inv_temp = ka.inv_temp;
+  c2.inv_bc1 = ka.inv_bc1;
+  c2.inv_bc2 = ka.inv_bc2;
+  c2.inv_ca = ka.inv_ca;
+  c2.inv_cb = ka.inv_cb;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
     const int64_t e = gi * 4;
     if constexpr (NOISE == BDL_NOISE_PHILOX) ep[u] = step_noise4(a, gi);
     StepConst cc;  // collect_core only reads inv_ca / inv_cb
-    cc.inv_ca = c.inv_ca;
-    cc.inv_cb = c.inv_cb;
+    cc.inv_ca = c2.inv_ca;
+    cc.inv_cb = c2.inv_cb;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float xt = th[u][j], xg = g[u][j], xvm = vm[u][j], xm = m[u][j], xv = v[u][j],
             xb = buf[u][j], x1 = m1[u][j], x2 = m2[u][j];
-      adam_core<NOISE, RECIP, PRIOR, GRADONLY>(a, c, eta, xt, xg, xvm, xm, xv, xb, t0[u][j],
+      adam_core<NOISE, RECIP, PRIOR, GRADONLY>(ka, c2, eta, xt, xg, xvm, xm, xv, xb, t0[u][j],
                                                ep[u][j]);
-      collect_core<COLLECT, RECIP>(a, cc, xt, x1, x2);
+      collect_core<COLLECT, RECIP>(ka, cc, xt, x1, x2);
       th[u][j] = xt;
       g[u][j] = xg;
       vm[u][j] = xvm;
@@ -1340,7 +1599,7 @@ StepKernel pick_unroll(int unroll) {
   // production kernels; the *_GRAD and test-only noise-free variants use the
   // default depth to keep build time down.
   constexpr bool kAllDepths =
-      METHOD == BDL_CSGHMC ||
+      is_csghmc_sweep<METHOD>() ||
       ((METHOD == BDL_SGLD || METHOD == BDL_SGHMC) && NOISE != BDL_NOISE_NONE);
   if constexpr (!kAllDepths) {
     (void)unroll;
@@ -1388,6 +1647,7 @@ StepKernel pick_noise(int noise, int collect, int unroll) {
 }
 
 StepKernel pick_step_csghmc(int noise, int collect, int unroll);
+StepKernel pick_step_csghmc_bare(int collect, int unroll);
 StepKernel pick_step_sghmc(int method, int noise, int collect, int unroll);
 StepKernel pick_step_sgld(int method, int noise, int collect, int unroll);
 StepKernel pick_adam(int noise, int collect, bool grad_only, int unroll);

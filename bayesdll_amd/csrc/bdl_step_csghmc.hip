@@ -7,4 +7,9 @@ StepKernel pick_step_csghmc(int noise, int collect, int unroll) {
   return pick_noise<BDL_CSGHMC>(noise, collect, unroll);
 }
 
+// the same sweeps with the arithmetic removed (bdl_sgmcmc_step_bare)
+StepKernel pick_step_csghmc_bare(int collect, int unroll) {
+  return pick_collect<kMethodBare, BDL_NOISE_NONE>(collect, unroll);
+}
+
 }  // namespace bdl

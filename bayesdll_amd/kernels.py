@@ -198,6 +198,18 @@ def sgmcmc_step(state, method, **kw):
                                    "bdl_sgmcmc_step"), a, written=wr)
 
 
+def sgmcmc_step_bare(state, **kw):
+    """The cSGHMC step of these arguments with its arithmetic removed
+    (bdl_sgmcmc_step_bare, include/bdl_measure.h): measurement only — the
+    production kernel's own loop, loads and stores, at the launch
+    configuration currently installed (set_launch_config; no tuning, no
+    geometry switch).  theta / mom / steady-state moments keep their values.
+    Asynchronous."""
+    a = _step_args(state, L.CSGHMC, **kw)
+    L.check(L.lib().bdl_sgmcmc_step_bare(a, L.current_stream_handle(state.device)),
+            "bdl_sgmcmc_step_bare")
+
+
 def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps, t,
               momentum_decay, nd, temperature=1.0, grad_is_mom=False, lrs, noise_mode,
               sigma2, n_data, mu=0.0, first_step=False, momentum=False, collect=L.COLLECT_NONE,
@@ -235,16 +247,18 @@ def adam_step(state, method, *, adam_m, adam_v, sgd_buf=None, beta1, beta2, eps,
                                    "bdl_adam_step"), a, ad, written=wr)
 
 
-def stream_mix(reads, writes, blocks_per_cu=1, unroll=4):
-    """The bare access mix of a sweep over these buffers (bdl_stream_mix,
-    include/bdl_measure.h): measurement only — the written tensors' contents
-    are destroyed.  Asynchronous, on the current stream."""
+def stream_mix(reads, writes, blocks_per_cu=1, unroll=4, schedule=L.MIX_BARE):
+    """The bare access mix of a sweep over these buffers in one issue schedule
+    (bdl_stream_mix_schedule, include/bdl_measure.h: L.MIX_BARE, MIX_PIPELINED,
+    MIX_PACED): measurement only — the written tensors' contents are
+    destroyed.  Asynchronous, on the current stream."""
     n = reads[0].numel()
     dev = reads[0].device
     rp = (C.c_void_p * len(reads))(*[t.data_ptr() for t in reads])
     wp = (C.c_void_p * len(writes))(*[t.data_ptr() for t in writes])
-    L.check(L.lib().bdl_stream_mix(rp, len(reads), wp, len(writes), int(n), int(blocks_per_cu),
-                                   int(unroll), L.current_stream_handle(dev)), "bdl_stream_mix")
+    L.check(L.lib().bdl_stream_mix_schedule(rp, len(reads), wp, len(writes), int(n),
+                                            int(blocks_per_cu), int(unroll), int(schedule),
+                                            L.current_stream_handle(dev)), "bdl_stream_mix")
 
 
 def clip_workspace(state):

@@ -258,23 +258,48 @@ def rank_devices(dist, local, world):
 MIX_GEOMS = ((1, 4), (2, 4), (2, 2), (3, 4), (4, 2), (1, 1), (2, 1), (4, 1))
 
 
-def mix_ceiling(reads, writes, same, kernel_ms, reps=8):
+MIX_SCHEDULES = (("bare", 0), ("pipelined", 1), ("paced", 2))  # include/bdl_measure.h
+
+
+def mix_ceiling(reads, writes, same, kernel_ms, reps=8, step=None):
     """The HBM ceiling of a kernel's exact access pattern on its exact buffers:
-    the bare mix (bdl_stream_mix — the same streams read and written, no
-    arithmetic, the step kernels' loop shape) at the kernel's own launch
-    geometry and at the best of MIX_GEOMS.  `of_ceiling` = best bare mix time /
-    kernel time.  Destroys the written vectors' contents: run last."""
+    the access mix (bdl_stream_mix_schedule — the same streams read and
+    written, no update arithmetic, the step kernels' loop shape) in each issue
+    schedule (bare: loads then stores; pipelined: the next iteration's loads
+    before this one's stores; paced: a Philox draw per group between loads
+    and stores) at every geometry of MIX_GEOMS.  The ceiling is the fastest of
+    them (the memory system does not serve every order of the same bytes
+    equally fast); `of_ceiling` = ceiling time / kernel time, `same_geometry_ms`
+    the bare mix at the kernel's own geometry.  `step` (cSGHMC sweeps): a
+    launcher of the kernel's own sweep with its arithmetic removed
+    (bdl_sgmcmc_step_bare), timed at every geometry too ("step_shaped": the
+    production loop, run table and load / store order).  Destroys the written
+    vectors' contents: run last."""
     from bayesdll_amd import kernels as K
 
-    def t(bpc, u):
-        return float(np.mean(event_times(lambda i: K.stream_mix(reads, writes, bpc, u), reps,
+    def t(bpc, u, s):
+        return float(np.mean(event_times(lambda i: K.stream_mix(reads, writes, bpc, u, s), reps,
                                          warm=2)))
-    same_ms = t(*same)
-    best = min((t(b, u), (b, u)) for b, u in MIX_GEOMS)
+    same_ms = t(*same, 0)
+    per = {}
+    for name, s in MIX_SCHEDULES:
+        per[name] = min((t(b, u, s), (b, u)) for b, u in MIX_GEOMS)
+    if step is not None:
+        prev = K._ACTIVE[0]
+        best = None
+        for b, u in MIX_GEOMS:
+            K.set_launch_config(b, u, 1)
+            ms = float(np.mean(event_times(lambda i: step(), reps, warm=2)))
+            best = min(best, (ms, (b, u))) if best else (ms, (b, u))
+        K.set_launch_config(*(prev or (0, 0, 0)))
+        per["step_shaped"] = best
+    bname, (bms, bg) = min(per.items(), key=lambda kv: kv[1][0])
     return {"mix": f"{len(reads)} reads, {len(writes)} writes", "kernel_ms": round(kernel_ms, 4),
-            "same_geometry_ms": round(same_ms, 4), "best_ms": round(best[0], 4),
-            "best_geometry": f"{best[1][0]}wg/cu x{best[1][1]}",
-            "of_ceiling": round(best[0] / kernel_ms, 4)}
+            "same_geometry_ms": round(same_ms, 4), "best_ms": round(bms, 4),
+            "best_geometry": f"{bg[0]}wg/cu x{bg[1]}", "best_schedule": bname,
+            "schedules": {k: {"best_ms": round(v[0], 4), "geometry": f"{v[1][0]}wg/cu x{v[1][1]}"}
+                          for k, v in per.items()},
+            "of_ceiling": round(bms / kernel_ms, 4)}
 
 
 def aux_kernels(st, reps=20):
@@ -1028,10 +1053,13 @@ def main():
     manual = (max(a.blocks_per_cu, 1), max(a.unroll, 1), 1)
     cfg = (st.launch_cfg or manual) if launch.get("autotuned") else manual
     ccfg = (st.collect_cfg or cfg) if launch.get("autotuned") else manual
+    bare_kw = dict(lrs=(1e-5, 1e-3), noise_scale=(0.0, 0.0), noise_mode=L.NOISE_NONE,
+                   one_minus_alpha=1 - 0.18, prior_sig=1.0)
     if not adam:
         rd = [st.theta, st.grad] + ([st.prior] if sgld else []) + [st.mom]
-        out["roofline"]["mix_ceiling"] = mix_ceiling(rd, [st.theta, st.mom], cfg[:2],
-                                                     dom["avg_ms"])
+        out["roofline"]["mix_ceiling"] = mix_ceiling(
+            rd, [st.theta, st.mom], cfg[:2], dom["avg_ms"],
+            step=None if sgld else (lambda: K.sgmcmc_step_bare(st, **bare_kw)))
     else:
         ex = st.extra
         out["roofline"]["mix_ceiling"] = mix_ceiling(
@@ -1042,14 +1070,18 @@ def main():
         if "collect_steady" in table:
             table["collect_steady"]["mix_ceiling"] = mix_ceiling(
                 [st.theta, st.grad, st.mom, cm1, cm2], [st.theta, st.mom, cm1, cm2], ccfg[:2],
-                table["collect_steady"]["avg_ms"])
+                table["collect_steady"]["avg_ms"],
+                step=lambda: K.sgmcmc_step_bare(st, collect=L.COLLECT_WELFORD, mom1=cm1, mom2=cm2,
+                                                collect_a=3.0, **bare_kw))
         ci = (out.get("aux_kernels") or {}).get("collect_init")
         if ci is not None:
             icfg = (getattr(st, "init_cfg", None) or cfg) if launch.get("autotuned") else manual
             c0 = min(m1s)  # the pair collect_init_timing ran on (placement differs per pair)
-            ci["mix_ceiling"] = mix_ceiling([st.theta, st.grad, st.mom],
-                                            [st.theta, st.mom, m1s[c0], m2s[c0]], icfg[:2],
-                                            ci["avg_ms"])
+            ci["mix_ceiling"] = mix_ceiling(
+                [st.theta, st.grad, st.mom], [st.theta, st.mom, m1s[c0], m2s[c0]], icfg[:2],
+                ci["avg_ms"],
+                step=lambda: K.sgmcmc_step_bare(st, collect=L.COLLECT_WELFORD_INIT, mom1=m1s[c0],
+                                                mom2=m2s[c0], collect_a=1.0, **bare_kw))
     del st, m1s, m2s
     torch.cuda.empty_cache()
     if world == 1 and not sgld and not a.no_methods:

@@ -10,6 +10,8 @@
 
 #include <stdint.h>
 
+#include "bdl_sgmcmc.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -27,6 +29,33 @@ extern "C" {
 int bdl_stream_mix(const float* const* reads, int32_t nreads, float* const* writes,
                    int32_t nwrites, int64_t n, int32_t blocks_per_cu, int32_t unroll,
                    void* hip_stream);
+
+/* The cSGHMC step launch of `args` (bdl_sgmcmc_step, include/bdl_sgmcmc.h;
+ * method BDL_CSGHMC, any collect kind) at the current launch configuration,
+ * with the update arithmetic and the noise draw removed: the production
+ * kernel's own loop, run table, loads and stores.  theta, mom and (steady
+ * kinds) mom1 / mom2 are written back as loaded; the init kinds write
+ * mom1 = theta and mom2 = 0 (Welford) or theta^2 (running mean), as the
+ * step does.  Its time is the ceiling of that kernel's access schedule.
+ * BDL_ERR_ARG for another method. */
+int bdl_sgmcmc_step_bare(const bdl_step_args* args, void* hip_stream);
+
+/* Issue schedules of the mix (bdl_stream_mix_schedule): the ceiling of an
+ * access pattern is the fastest of them, since the memory system does not
+ * serve every order of the same bytes equally fast. */
+typedef enum bdl_mix_schedule {
+  BDL_MIX_BARE = 0,      /* each iteration: all its loads, then all its stores (bdl_stream_mix) */
+  BDL_MIX_PIPELINED = 1, /* the next iteration's loads issued before this one's stores          */
+  BDL_MIX_PACED = 2      /* BARE with one Philox4x32-10 + Box-Muller draw per float4 group
+                            between loads and stores (a noise-bearing sweep's arithmetic,
+                            weighted 0 in the written value)                                 */
+} bdl_mix_schedule;
+
+/* bdl_stream_mix in one of the schedules above; same streams, sizes,
+ * geometry and written values.  BDL_ERR_ARG for an unknown schedule. */
+int bdl_stream_mix_schedule(const float* const* reads, int32_t nreads, float* const* writes,
+                            int32_t nwrites, int64_t n, int32_t blocks_per_cu, int32_t unroll,
+                            int32_t schedule, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -21,7 +21,8 @@ def declared_functions(headers=HEADERS):
 
 
 def test_header_declares_expected_api():
-    assert declared_functions([HEADERS[1]]) == ["bdl_stream_mix"]
+    assert declared_functions([HEADERS[1]]) == ["bdl_sgmcmc_step_bare", "bdl_stream_mix",
+                                                "bdl_stream_mix_schedule"]
     assert declared_functions([HEADERS[2]]) == sorted([
         "bdl_arena_reserve", "bdl_arena_alloc", "bdl_arena_free", "bdl_arena_stats",
         "bdl_arena_contains"])
@@ -234,6 +235,9 @@ def test_other_entry_points_refuse_while_a_graph_redirect_is_active():
             "bdl_philox_normal": lambda: h.bdl_philox_normal(C.c_void_p(0x1000), 8, 0, 0, 0, None),
             "bdl_stream_mix": lambda: h.bdl_stream_mix((C.c_void_p * 1)(0x1000), 1,
                                                        (C.c_void_p * 1)(0x2000), 1, 8, 1, 1, None),
+            "bdl_sgmcmc_step_bare": lambda: h.bdl_sgmcmc_step_bare(a, None),
+            "bdl_stream_mix_schedule": lambda: h.bdl_stream_mix_schedule(
+                (C.c_void_p * 1)(0x1000), 1, (C.c_void_p * 1)(0x2000), 1, 8, 1, 1, 2, None),
         }
         for name, call in calls.items():
             assert call() == -3, name

@@ -775,18 +775,67 @@ def test_posterior_draw_geometry_changes_nothing_and_is_tuned_once():
 
 @pytest.mark.parametrize("nr,nw", [(2, 1), (3, 2), (4, 2), (3, 4), (5, 4), (7, 5)])
 def test_stream_mix_writes_the_first_read_stream(nr, nw):
-    """bdl_stream_mix (the bench's bare access-mix ceiling): every written
-    vector receives reads[0] (+ 0 x the others), at a ragged size and three
-    geometries; unsupported mixes are refused."""
+    """bdl_stream_mix_schedule (the bench's access-mix ceiling): in every issue
+    schedule, every written vector receives reads[0] (+ 0 x the others), at a
+    ragged size and three geometries (the pipelined schedule's iteration
+    counts differ per block); unsupported mixes and schedules are refused."""
+    from bayesdll_amd import _lib as L
     from bayesdll_amd import kernels as K
     n = 3 * (1 << 18) + 5
     g = torch.Generator(device=DEV).manual_seed(nr * 10 + nw)
     reads = [torch.randn(n, device=DEV, generator=g) for _ in range(nr)]
-    for bpc, u in ((1, 4), (2, 2), (3, 1)):
-        writes = [torch.full((n,), 7.0, device=DEV) for _ in range(nw)]
-        K.stream_mix(reads, writes, bpc, u)
-        torch.cuda.synchronize()
-        for w in writes:
-            assert torch.equal(w, reads[0])
+    for sched in (L.MIX_BARE, L.MIX_PIPELINED, L.MIX_PACED):
+        for bpc, u in ((1, 4), (2, 2), (3, 1)):
+            writes = [torch.full((n,), 7.0, device=DEV) for _ in range(nw)]
+            K.stream_mix(reads, writes, bpc, u, schedule=sched)
+            torch.cuda.synchronize()
+            for w in writes:
+                assert torch.equal(w, reads[0]), (sched, bpc, u)
     with pytest.raises(RuntimeError, match="supported"):
         K.stream_mix(reads[:1] * 6, [reads[0]], 1, 4)
+    with pytest.raises(RuntimeError, match="schedule"):
+        K.stream_mix(reads, [torch.empty_like(reads[0])] * nw, 1, 4, schedule=3)
+
+
+@pytest.mark.parametrize("unroll", [1, 2, 4])
+def test_bare_step_keeps_values_and_copies_the_init_moments(unroll):
+    """bdl_sgmcmc_step_bare (the bench's step-shaped ceiling): the cSGHMC
+    sweep of every collect kind with its arithmetic removed writes theta, mom
+    and the steady-state moments back unchanged and the init moments as the
+    step does (Welford m1 = theta, m2 = 0; running mean m1 = theta, m2 =
+    theta^2), over a ragged many-run state at each unroll depth (fast,
+    multi-run and guarded iterations); other methods are refused."""
+    from bayesdll_amd import _lib as L
+    from bayesdll_amd import kernels as K
+    segs = [(f"layer{i}.weight", (3 + 5 * i, 7 + i)) for i in range(37)] + [("fc.weight", (10, 33)),
+                                                                        ("fc.bias", (10,))]
+    st = _state(segs, "fc", need_noise=True)
+    K.set_launch_config(2, unroll, 1)
+    try:
+        th0, v0 = st.theta.clone(), st.mom.clone()
+        kw = dict(lrs=(1e-3, 1e-2), noise_scale=(0.0, 0.0), noise_mode=L.NOISE_NONE,
+                  one_minus_alpha=0.9, prior_sig=1.0)
+        K.sgmcmc_step_bare(st, **kw)
+        m1 = torch.randn_like(st.theta)
+        m2 = torch.rand_like(st.theta)
+        a1, a2 = m1.clone(), m2.clone()
+        for collect in (L.COLLECT_WELFORD, L.COLLECT_MEAN):
+            K.sgmcmc_step_bare(st, collect=collect, mom1=m1, mom2=m2, collect_a=3.0,
+                               collect_b=4.0, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(st.theta, th0) and torch.equal(st.mom, v0)
+        assert torch.equal(m1, a1) and torch.equal(m2, a2)
+        K.sgmcmc_step_bare(st, collect=L.COLLECT_WELFORD_INIT, mom1=m1, mom2=m2, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(m1, th0) and torch.equal(m2, torch.zeros_like(m2))
+        K.sgmcmc_step_bare(st, collect=L.COLLECT_MEAN_INIT, mom1=m1, mom2=m2, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(m1, th0) and torch.equal(m2, th0 * th0)
+        assert torch.equal(st.theta, th0) and torch.equal(st.mom, v0)
+    finally:
+        K.set_launch_config(0, 0, 0)
+    st2 = _state(segs, "fc", need_prior=True)
+    a = K._step_args(st2, L.SGLD, lrs=(1e-3, 1e-2), noise_scale=(0.0, 0.0),
+                     noise_mode=L.NOISE_NONE)
+    with pytest.raises(RuntimeError, match="cSGHMC only"):
+        L.check(L.lib().bdl_sgmcmc_step_bare(a, None), "bdl_sgmcmc_step_bare")

@@ -9,7 +9,8 @@ ROUNDS rounds — so a build's number is never a different allocation's number.
   separate allocations (the Runners' default); GRAD=views: the same table over
   views of the one flat gradient allocation; GRAD=ab: flat and per-tensor
   gradients alternating in the same process (reported as lib name + "/flat"
-  and "/tensor").
+  and "/tensor").  COLLECT_ALL=1: the collect step at every geometry (default:
+  the first only).
 """
 import json
 import os
@@ -32,9 +33,21 @@ dev = torch.device("cuda", 0)
 
 
 def use(path):
+    """Load one build; an older build (the A/B baseline) may lack entry points
+    added since, which this tool never calls: they are left unbound."""
+    import ctypes
     L._lib = None
     L.LIB_PATH = path
-    L.lib()
+    h = ctypes.CDLL(path)
+    saved = dict(L.EXPORTS)
+    for name in list(L.EXPORTS):
+        if not hasattr(h, name):
+            del L.EXPORTS[name]
+    try:
+        L.lib()
+    finally:
+        L.EXPORTS.clear()
+        L.EXPORTS.update(saved)
 
 
 METHOD = os.environ.get("METHOD", "csghmc")  # or "adam" (Adam-SGHMC + SGD), "sgld" (+ SGD),
@@ -53,6 +66,7 @@ m1 = st.theta.clone()
 m2 = torch.zeros_like(st.theta)
 n = st.n
 GRAD = os.environ.get("GRAD", "flat")
+COLLECT_ALL = os.environ.get("COLLECT_ALL", "0") == "1"  # the collect at every geometry
 _flat = st.grad
 _grads = [st.grad[o:o + k].clone() for o, k in zip(st.offsets, st.numels)] \
     if GRAD in ("tensor", "ab") else None
@@ -119,6 +133,16 @@ def collect(i):
                   mom2=m2, collect_a=float(i + 3), seed=3, chain=0, step=i)
 
 
+def init(i):  # the cycle-init Welford collect (csghmc.py:333-337): m1 = theta, m2 = 0
+    ns = [0.01 * np.sqrt(2 * alpha * x) / N for x in lrs]
+    K.sgmcmc_step(st, L.CSGHMC, lrs=lrs, noise_scale=ns, noise_mode=L.NOISE_PHILOX,
+                  one_minus_alpha=1 - alpha, prior_sig=1.0, collect=L.COLLECT_WELFORD_INIT,
+                  mom1=m1, mom2=m2, collect_a=1.0, seed=3, chain=0, step=i)
+
+
+INIT = os.environ.get("INIT", "0") == "1" and METHOD == "csghmc"  # also time the init collect
+
+
 def t(fn, reps=20):
     for i in range(3):
         fn(i)
@@ -145,8 +169,10 @@ for r in range(rounds):
             for name, fn, bpe in ((METHOD if METHOD in ("adam", "sgld", "sghmc", "draw")
                                    else "explore", explore,
                                    {"adam": 48, "sgld": 24, "sghmc": 24, "draw": 12}.get(METHOD, 20)),
-                                  ("collect", collect, 40 if sgld or sghmc else 36)):
-                if name == "collect" and (g != geoms[0] or adam or METHOD == "draw"):
+                                  ("collect", collect, 40 if sgld or sghmc else 36)) + \
+                    ((("init", init, 28),) if INIT else ()):
+                if name in ("collect", "init") and (adam or METHOD == "draw" or
+                                          (g != geoms[0] and not COLLECT_ALL)):
                     continue
                 ms = t(fn)
                 res.setdefault((tag, g, name), []).append(ms)
