@@ -761,151 +761,6 @@ __device__ __forceinline__ void chunk_multi(const A& a, const StepConst& c, int6
   }
 }
 
-// ---------------------------------------------------------------------------
-// Software-pipelined cSGHMC collect sweep (sample steps that update the
-// posterior moments: Welford init, Welford, running-mean collects): the next
-// block iteration's loads are issued before this iteration's Philox draw,
-// update and stores, so at one wave per SIMD — the geometry the collects
-// tune to — the draw no longer sits between a load's return and the next
-// load's issue.  Two register sets take turns (the loop body written twice
-// with the roles swapped); an iteration that needs the multi-run or guarded
-// path drains the pipeline.  Same per-element update as chunk_fast (PRIOR and
-// GR never apply to cSGHMC), so results are bit-identical.
-// ---------------------------------------------------------------------------
-template <int COLLECT>
-constexpr bool pipe_csghmc_collect() {
-#ifdef BDL_PIPE_CSGHMC_COLLECT
-  return COLLECT != BDL_COLLECT_NONE;
-#else
-  return false;
-#endif
-}
-
-template <int U>
-struct CsgRegs {
-  f4v th[U], g[U], v[U], m1[U], m2[U];
-};
-
-template <int COLLECT, int U>
-__device__ __forceinline__ void csg_pipe_load(const KArgs& a, const StepConst& c, int64_t gb,
-                                              const float* gp, CsgRegs<U>& R) {
-  constexpr bool kReadMoments = COLLECT == BDL_COLLECT_WELFORD || COLLECT == BDL_COLLECT_MEAN;
-  const f4v z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t e = (gb + (int64_t)u * kBlock + threadIdx.x) * 4;
-    R.th[u] = vload(a.theta + e);
-    R.g[u] = vload(gp + e);
-    R.v[u] = vload(a.mom + e);
-    R.m1[u] = R.m2[u] = z;
-    if constexpr (kReadMoments) {
-      R.m1[u] = vload(a.mom1 + e);
-      if (c.has_m2) R.m2[u] = vload(a.mom2 + e);
-    }
-  }
-}
-
-template <int NOISE, int COLLECT, bool RECIP, int U>
-__device__ __forceinline__ void csg_pipe_compute(const KArgs& a, const StepConst& c, int64_t gb,
-                                                 float eta, float ns, CsgRegs<U>& R,
-                                                 uint32_t& bad) {
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
-    const int64_t e = gi * 4;
-    f4v ep = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (NOISE == BDL_NOISE_PHILOX) ep = step_noise4(a, gi);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float xt = R.th[u][j], xg = R.g[u][j], xv = R.v[u][j], x1 = R.m1[u][j], x2 = R.m2[u][j];
-      update_core<BDL_CSGHMC, NOISE, RECIP, false, false>(a, c, eta, ns, xt, xg, xv, 0.f, ep[j]);
-      collect_core<COLLECT, RECIP>(a, c, xt, x1, x2);
-      R.th[u][j] = xt;
-      R.v[u][j] = xv;
-      R.m1[u][j] = x1;
-      R.m2[u][j] = x2;
-    }
-    bad |= nonfinite4(R.th[u]);
-    vstore(a.theta + e, R.th[u]);
-    vstore(a.mom + e, R.v[u]);
-    vstore(a.mom1 + e, R.m1[u]);
-    if (c.has_m2) vstore(a.mom2 + e, R.m2[u]);
-  }
-}
-
-// Cursor of the pipelined sweep: the block iteration, its run, whether it
-// takes the fast path and whether its data already sit in the current set.
-struct CsgCursor {
-  int64_t gb;
-  int r;
-  uint32_t attr;
-  bool fast, loaded;
-};
-
-template <int U>
-__device__ __forceinline__ bool csg_pipe_fast(const KArgs& a, int64_t gb, int64_t g1, int& r,
-                                              uint32_t& attr) {
-  constexpr int64_t kIter = (int64_t)kBlock * U;
-  if (gb >= g1) return false;
-  while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
-  attr = run_attr(r);
-  const int64_t gend = gb + kIter;
-  return gend <= g1 && gend <= (a.n >> 2) && run_end(r) >= gend * 4 && !(attr & kNoFastPath);
-}
-
-// One block iteration with X as the current register set and Y as the next;
-// false when the block's span is done.
-template <int NOISE, int COLLECT, bool RECIP, int U>
-__device__ __forceinline__ bool csg_pipe_iter(const KArgs& a, const StepConst& c, int64_t g1,
-                                              int64_t gstep, CsgCursor& k, CsgRegs<U>& X,
-                                              CsgRegs<U>& Y, uint32_t& bad) {
-  constexpr int64_t kIter = (int64_t)kBlock * U;
-  if (k.gb >= g1) return false;
-  if (!k.fast) {
-    const int64_t gend = min(k.gb + kIter, g1);
-    if (gend == k.gb + kIter && gend <= (a.n >> 2) && multi_run_ok(a.nruns, k.r, gend * 4))
-      chunk_multi<BDL_CSGHMC, NOISE, COLLECT, RECIP, U>(a, c, k.gb, k.r, bad);
-    else
-      chunk_slow<BDL_CSGHMC, NOISE, COLLECT, RECIP, U>(a, c, k.gb, gend, k.r, bad);
-    k.gb += gstep;
-    k.fast = csg_pipe_fast<U>(a, k.gb, g1, k.r, k.attr);
-    k.loaded = false;
-    return true;
-  }
-  if (!k.loaded) csg_pipe_load<COLLECT, U>(a, c, k.gb, run_grad(a, k.r), X);
-  // the next iteration: classify it and issue its loads before this one's math
-  const int64_t nx = k.gb + gstep;
-  int rn = k.r;
-  uint32_t attrn = 0;
-  const bool fastn = csg_pipe_fast<U>(a, nx, g1, rn, attrn);
-  if (fastn) csg_pipe_load<COLLECT, U>(a, c, nx, run_grad(a, rn), Y);
-  const bool head = (k.attr & BDL_ATTR_HEAD) != 0;
-  csg_pipe_compute<NOISE, COLLECT, RECIP, U>(a, c, k.gb, head ? a.lr1 : a.lr0,
-                                             head ? a.ns1 : a.ns0, X, bad);
-  k.gb = nx;
-  k.r = rn;
-  k.attr = attrn;
-  k.fast = fastn;
-  k.loaded = fastn;
-  return true;
-}
-
-template <int NOISE, int COLLECT, bool RECIP, int U>
-__device__ __forceinline__ void csg_pipe_sweep(const KArgs& a, const StepConst& c, int64_t g0,
-                                               int64_t g1, int64_t gstep, int r, uint32_t& bad) {
-  CsgCursor k;
-  k.gb = g0;
-  k.r = r;
-  k.attr = 0;
-  k.fast = csg_pipe_fast<U>(a, k.gb, g1, k.r, k.attr);
-  k.loaded = false;
-  CsgRegs<U> A, B;
-  for (;;) {
-    if (!csg_pipe_iter<NOISE, COLLECT, RECIP, U>(a, c, g1, gstep, k, A, B, bad)) break;
-    if (!csg_pipe_iter<NOISE, COLLECT, RECIP, U>(a, c, g1, gstep, k, B, A, bad)) break;
-  }
-}
-
 // Variants of a step body, fixed per launch (step_variant): the SGD step on
 // an already formed gradient (BDL_FLAG_GRAD_READY) and the clipped SGLD
 // gradient (bdl_sgld_step_clipped); kVarRuntime reads both from the launch.
@@ -969,10 +824,7 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
   // per-iteration run lookup, which needs fewer registers (with the per-run
   // loop: SGLD SGPR spills 0 -> 2-14 and ResNet-101 SGLD at 2 x 1 0.1793 vs
   // 0.1716 ms; cSGHMC depth-4 collects 0 -> 2-6 spills).
-  if constexpr (METHOD == BDL_CSGHMC && NOISE != BDL_NOISE_BUFFER &&
-                pipe_csghmc_collect<COLLECT>()) {
-    csg_pipe_sweep<NOISE, COLLECT, RECIP, UNROLL>(a, c, g0, g1, gstep, r, bad);
-  } else if constexpr (fresh_step_args<METHOD, NOISE, COLLECT, UNROLL>()) {
+  if constexpr (fresh_step_args<METHOD, NOISE, COLLECT, UNROLL>()) {
   for (int64_t gb = g0; gb < g1; gb += gstep) {
     // the iteration's arguments, flags included, from the re-read view
     ckargs& fa = fresh_kargs();
