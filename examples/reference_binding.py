@@ -1,7 +1,7 @@
 """The reference-side binding a maintainer would add to BayesDLL's
 methods/csghmc.py to run its per-tensor cSGHMC update (methods/csghmc.py:747-778)
 through the fused MI355X kernel — ctypes over include/bdl_sgmcmc.h, ABI
-version 6.  INTEGRATION.md §3 shows this file verbatim; tests/test_abi.py
+version 8.  INTEGRATION.md §3 shows this file verbatim; tests/test_abi.py
 checks its struct against the C header and the shipped library, and
 tests/test_gpu_reference_binding.py runs it against the product's own binding
 (bit for bit).
@@ -36,7 +36,7 @@ class Run(C.Structure):          # bdl_run
     _fields_ = [("end", C.c_int64), ("attr", C.c_uint32), ("pad", C.c_uint32)]
 
 
-class StepArgs(C.Structure):     # bdl_step_args, ABI v6
+class StepArgs(C.Structure):     # bdl_step_args, ABI v8
     _fields_ = [(f, C.c_void_p) for f in
                 ("theta", "grad", "mom", "prior_mean", "noise", "mom1", "mom2", "runs")] + [
         ("nruns", C.c_int32), ("method", C.c_int32), ("noise_mode", C.c_int32),

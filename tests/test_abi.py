@@ -490,7 +490,11 @@ def test_integration_snippet_is_the_tested_reference_binding():
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     assert open(path).read() in doc
     from bayesdll_amd import _lib as L
-    assert f"ABI version {L.ABI_VERSION}" in doc and f"ABI version {L.ABI_VERSION - 1}" not in doc
+    assert f"ABI version {L.ABI_VERSION}" in doc
+    for old in range(1, L.ABI_VERSION):  # no stale version number in the doc or the binding
+        for text in (doc, open(path).read()):
+            assert f"ABI version {old}" not in text and f"ABI v{old}," not in text
+            assert not re.search(rf"ABI\s+version {old}\b", text), old
 
 
 def test_reference_binding_struct_matches_header_and_library():

@@ -112,3 +112,34 @@ def test_distinct_device_check_refuses_shared_or_missing_gpus():
     shared = ids[:7] + [dict(ids[3])]
     assert "same GPU" in b.check_distinct_devices(shared, "nccl", 8, 8)
     assert b.check_distinct_devices([ids[0]] * 8, "gloo", 1, 8) is None
+
+
+def test_rank_devices_exits_3_when_ranks_share_a_gpu(monkeypatch):
+    """bench.rank_devices under RCCL: ranks that report one GPU, or a node
+    that shows fewer GPUs than ranks, end the run with exit status 3 (after
+    tearing the process group down) before anything is timed."""
+    import pytest
+    import torch
+    b = _bench_module()
+
+    class FakeDist:
+        destroyed = 0
+
+        def all_gather_object(self, out, obj):
+            for i in range(len(out)):
+                out[i] = dict(obj)  # every rank reports the same device
+
+        def get_backend(self):
+            return "nccl"
+
+        def destroy_process_group(self):
+            FakeDist.destroyed += 1
+
+    monkeypatch.setattr(b, "device_identity",
+                        lambda local: {"index": local, "pci": "0000:05:00.0", "uuid": "GPU-0"})
+    for ndev in (8, 1):  # shared device; fewer devices than ranks
+        monkeypatch.setattr(torch.cuda, "device_count", lambda: ndev)
+        with pytest.raises(SystemExit) as e:
+            b.rank_devices(FakeDist(), 0, 2)
+        assert e.value.code == 3
+    assert FakeDist.destroyed == 2

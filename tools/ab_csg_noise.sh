@@ -4,6 +4,8 @@
 # through the global address space (F=gv, -DBDL_CSG_COLLECT_GVLOAD) vs the
 # Philox inputs waited for before the vector loads (F=pf,
 # -DBDL_CSG_PHILOX_FIRST) — same process, builds alternating (tools/step_ab.py).
+# Both macros lived in bdl_kernels.hpp for this A/B only (not adopted, not
+# committed); results in profiles/round6/ab_csg_noise/.
 # Usage: bash tools/ab_csg_noise.sh LIB [LIB ...]
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
