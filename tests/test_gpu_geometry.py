@@ -10,25 +10,30 @@ pytestmark = pytest.mark.gpu
 GEOMETRIES = [(1, 1, 0), (1, 2, 1), (1, 4, 1), (2, 1, 1), (2, 4, 0), (3, 2, 1), (4, 4, 1)]
 
 
-def _state(n, seed):
+def _state(n, seed, need_noise=False):
     from bayesdll_amd import _lib as L
     from bayesdll_amd.flat import FlatState
     segs = [("body.weight", (n - 37,)), ("body.bias", (30,)), ("head.weight", (7,))]
-    st = FlatState.from_segments(segs, "head", device="cuda", need_mom=True, need_prior=True)
+    st = FlatState.from_segments(segs, "head", device="cuda", need_mom=True, need_prior=True,
+                                 need_noise=need_noise)
     g = torch.Generator(device="cuda").manual_seed(seed)
-    for v in (st.theta, st.grad, st.mom, st.prior):
+    for v in (st.theta, st.grad, st.mom, st.prior) + ((st.noise,) if need_noise else ()):
         v.copy_(torch.randn(st.n, device="cuda", generator=g))
     return st, L
 
 
-@pytest.mark.parametrize("method", ["csghmc", "sgld", "adam"])
+# sghmc / *_buffer: the instances that run on the re-read argument view at
+# depth 2 and 4 (bdl_kernels.hpp fresh_step_args) against their depth-1 form
+@pytest.mark.parametrize("method", ["csghmc", "sgld", "adam", "sghmc", "sgld_buffer",
+                                    "sghmc_buffer"])
 def test_results_do_not_depend_on_launch_geometry(method):
     from bayesdll_amd import kernels as K
     n = 3 * (1 << 20) + 13  # ragged: partial float4 group and partial block iterations
     outs = []
     try:
         for geo in GEOMETRIES:
-            st, L = _state(n, 1)
+            st, L = _state(n, 1, need_noise=method.endswith("_buffer"))
+            nmode = L.NOISE_BUFFER if method.endswith("_buffer") else L.NOISE_PHILOX
             m1 = torch.zeros(n, device="cuda")
             m2 = torch.zeros(n, device="cuda")
             K.set_launch_config(*geo)
@@ -49,9 +54,15 @@ def test_results_do_not_depend_on_launch_geometry(method):
                                 collect=L.COLLECT_MEAN if t else L.COLLECT_NONE, mom1=m1,
                                 mom2=m2, collect_a=float(t), collect_b=float(t + 1), seed=3,
                                 chain=1, step=t)
+                elif method.startswith("sghmc"):  # SGHMC + SGD(0) + running moments
+                    K.sgmcmc_step(st, L.SGHMC, lrs=(1e-3, 2e-3), noise_scale=(1e-2, 2e-2),
+                                  noise_mode=nmode, one_minus_alpha=0.9, sigma2=1.0,
+                                  n_data=100.0, collect=L.COLLECT_MEAN_INIT if t == 0 else
+                                  L.COLLECT_MEAN, mom1=m1, mom2=m2, collect_a=float(t + 1),
+                                  collect_b=float(t + 2), seed=3, chain=1, step=t)
                 else:
                     K.sgmcmc_step(st, L.SGLD, lrs=(1e-3, 2e-3), noise_scale=(1e-2, 2e-2),
-                                  noise_mode=L.NOISE_PHILOX, prior_sig=1.0, sigma2=1.0,
+                                  noise_mode=nmode, prior_sig=1.0, sigma2=1.0,
                                   n_data=100.0, mu=0.5, first_step=t == 0, momentum=True,
                                   collect=L.COLLECT_MEAN, mom1=m1, mom2=m2,
                                   collect_a=float(t + 1), collect_b=float(t + 2), seed=3,
