@@ -644,23 +644,34 @@ def e2e_steps(steps, warmup, local, seed, graph=False, overlap=False, arena=Fals
         model(x, y, net, None, crit, [1e-4, 1e-2], 1.0, 0.01, should_sample=(k % 10 == 0))
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
+    # the sampler's whole per-step cost, host side included: sampler steps and
     # the same forward + backward + loss.item() with no sampler at all (grads
-    # set to None as the sampler does): ms - this = everything the sampler adds
-    # per step, host side included, to compare with the update kernel's time
-    plain_ms = None
+    # set to None as the sampler does) alternate step by step, each step
+    # synchronised, so clock drift between the two legs cancels
+    plain_ms = sync_ms = None
     if not graph and not overlap:
         params = list(net.parameters())
-        for k in range(steps + 2):
-            if k == 2:
-                torch.cuda.synchronize()
-                t1 = time.perf_counter()
+
+        def plain():
             for p in params:
                 p.grad = None
             loss = crit(net(x), y)
             loss.backward()
             loss.item()
-        torch.cuda.synchronize()
-        plain_ms = (time.perf_counter() - t1) / steps * 1e3
+        ts = tp = 0.0
+        for k in range(steps + 2):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            model(x, y, net, None, crit, [1e-4, 1e-2], 1.0, 0.01, should_sample=(k % 10 == 0))
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            plain()
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            if k >= 2:
+                ts += t2 - t1
+                tp += t3 - t2
+        sync_ms, plain_ms = ts / steps * 1e3, tp / steps * 1e3
     # the update alone on the Runner's own gradients, after the timed steps
     # (HIP events around each launch; 9 explore + 1 sample step per 10, 20 B/elem)
     st.timer = K.StepTimer(1)
@@ -678,8 +689,9 @@ def e2e_steps(steps, warmup, local, seed, graph=False, overlap=False, arena=Fals
     return {"overlap_graphs": ovl_graphs, "rewrite_ms_per_step": rewrite_ms, "buckets": buckets,
             "steps_per_s": round(1e3 / ms, 2), "ms_per_step": round(ms, 3),
             "update_ms": round(upd["avg_ms"], 4) if upd.get("timed") else None,
+            "synchronised_ms_per_step": None if sync_ms is None else round(sync_ms, 3),
             "autograd_only_ms": None if plain_ms is None else round(plain_ms, 3),
-            "sampler_added_ms": None if plain_ms is None else round(ms - plain_ms, 3),
+            "sampler_added_ms": None if plain_ms is None else round(sync_ms - plain_ms, 3),
             "grad_arena": arena and not graph, "grads_in_arena": in_arena,
             "batch": [16, 3, 224, 224], "what": "ViT-L/32 fp32 fwd+bwd (autograd) + fused cSGHMC "
             "update, loss.item() sync per step as in the reference (informational)"}
