@@ -204,6 +204,18 @@ __device__ __forceinline__ ckargs& fresh_kargs() {
 // at [4*cgroups*k, 4*cgroups*(k+1))) chain k is keyed chain + k and draws what
 // a one-chain launch with that chain id draws.  The host keeps every group
 // index below 2^32 in that mode, so the split is a 32-bit division.
+// The Philox draw from the generator inputs of `a` as given.
+template <class A>
+__device__ __forceinline__ f4v noise_from(const A& a, int64_t gi) {
+  uint64_t g = (uint64_t)gi + a.goff, c = a.chain;
+  if (a.cgroups) {
+    const uint32_t k = (uint32_t)g / a.cgroups;
+    g -= (uint64_t)k * a.cgroups;
+    c += k;
+  }
+  return philox_normal4(g, a.seed, c, a.step);
+}
+
 template <class A>
 __device__ __forceinline__ f4v step_noise4(const A& a0, int64_t gi) {
 #ifdef BDL_PHILOX_KEYS_PER_CALL
@@ -216,17 +228,20 @@ __device__ __forceinline__ f4v step_noise4(const A& a0, int64_t gi) {
   typedef __attribute__((address_space(4))) const KArgs ckargs;
   ckargs* ap = (ckargs*)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(ap));
-  ckargs& a = *ap;
+  return noise_from(*ap, gi);
 #else
-  const A& a = a0;
+  return noise_from(a0, gi);
 #endif
-  uint64_t g = (uint64_t)gi + a.goff, c = a.chain;
-  if (a.cgroups) {
-    const uint32_t k = (uint32_t)g / a.cgroups;
-    g -= (uint64_t)k * a.cgroups;
-    c += k;
-  }
-  return philox_normal4(g, a.seed, c, a.step);
+}
+
+// HELD: the inputs as the caller's argument view holds them (no per-call
+// re-read; chunk_fast's kHeldNoise).
+template <bool HELD, class A>
+__device__ __forceinline__ f4v step_noise4_held(const A& a0, int64_t gi) {
+  if constexpr (HELD)
+    return noise_from(a0, gi);
+  else
+    return step_noise4(a0, gi);
 }
 
 // fl32(1/s64) from the caller, or 1/fl32(s) when it left the field 0
@@ -480,6 +495,17 @@ __device__ __forceinline__ void chunk_fast(const A& a, const StepConst& c, int64
                                            float eta, float ns, float* gp, uint32_t& bad) {
   using T = StepTraits<METHOD, COLLECT>;
   constexpr bool kPriorLoad = T::kReadPrior && PRIOR && !GR;
+  // the depth-1 SGLD / SGHMC collect instances draw their noise from the
+  // generator inputs held in SGPRs (the kernel's KArgs), not re-read per call:
+  // at one group per lane the per-call scalar loads' wait is one per group and
+  // sits in front of the draw.  Same process, builds alternating
+  // (profiles/round6/ab_held/): ResNet-101 SGLD collect 0.3042 ms at 1 x 1
+  // against the previous best 0.3107 (1 x 4), ViT-L/32 SGLD collect on
+  // per-tensor gradients 2.1473 vs 2.2072, SGHMC collect equal.  The plain
+  // depth-1 steps keep the per-call re-read: held, SGLD at its tuned 2 x 1 ran
+  // 0.1749 vs 0.1697 ms (its SGPR spills 0 -> 12).
+  constexpr bool kHeldNoise = UNROLL == 1 && COLLECT != BDL_COLLECT_NONE &&
+                              (METHOD == BDL_SGLD || METHOD == BDL_SGHMC);
   f4v th[UNROLL], g[UNROLL], v[UNROLL], t0[UNROLL], ep[UNROLL], m1[UNROLL], m2[UNROLL];
   const f4v z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -516,7 +542,7 @@ __device__ __forceinline__ void chunk_fast(const A& a, const StepConst& c, int64
     const int64_t gi = gb + (int64_t)u * kBlock + threadIdx.x;
     const int64_t e = gi * 4;
     if constexpr (NOISE == BDL_NOISE_PHILOX && !GR)
-      ep[u] = step_noise4(a, gi);
+      ep[u] = step_noise4_held<kHeldNoise>(a, gi);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float xt = th[u][j], xg = g[u][j], xv = v[u][j], x1 = m1[u][j], x2 = m2[u][j];
