@@ -204,7 +204,7 @@ __device__ __forceinline__ ckargs& fresh_kargs() {
 // at [4*cgroups*k, 4*cgroups*(k+1))) chain k is keyed chain + k and draws what
 // a one-chain launch with that chain id draws.  The host keeps every group
 // index below 2^32 in that mode, so the split is a 32-bit division.
-// The Philox draw from the generator inputs of `a` as given.
+// noise_from: the draw from the generator inputs of `a` as given.
 template <class A>
 __device__ __forceinline__ f4v noise_from(const A& a, int64_t gi) {
   uint64_t g = (uint64_t)gi + a.goff, c = a.chain;
@@ -223,9 +223,9 @@ __device__ __forceinline__ f4v step_noise4(const A& a0, int64_t gi) {
   // from the kernarg segment per call (scalar loads) instead of being held in
   // SGPRs across the sweep (see philox4x32_10).  Every kernel that draws
   // step noise takes its KArgs as the first kernel argument, at offset 0 of
-  // the segment.
+  // the segment.  (Spelled out rather than through fresh_kargs(): that form
+  // changed the Adam unit's register allocation, 34 -> 108 SGPR spills.)
   (void)a0;
-  typedef __attribute__((address_space(4))) const KArgs ckargs;
   ckargs* ap = (ckargs*)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(ap));
   return noise_from(*ap, gi);
