@@ -18,7 +18,13 @@ region; value = total chain-steps / max-over-ranks wall time.
 Prints one JSON line (rank 0).  Extra fields: hbm_gbs (algorithmic), the
 per-kernel-kind table with HIP-event timings, roofline of the dominant
 kernel, and the CPU baseline (the oracle's op-for-op torch-CPU restatement of
-the reference update, timed on this host on a bounded sample).
+the reference update, timed on this host on a bounded sample).  After the
+timed region (never inside it): every sweep's `mix_ceiling` (the fastest
+arithmetic-free form of its own access pattern on its own buffers: bare,
+pipelined, paced and, for cSGHMC, the kernel's own loop without its update),
+the explore on the Runners' per-tensor gradients, the other configurations'
+sweeps (`methods`), and end-to-end ViT-L/32 steps with an interleaved
+autograd-only leg (`e2e`, informational).
 """
 from __future__ import annotations
 
