@@ -792,6 +792,18 @@ __device__ __forceinline__ void chunk_multi(const A& a, const StepConst& c, int6
 // gradient (bdl_sgld_step_clipped); kVarRuntime reads both from the launch.
 constexpr int kVarGradReady = 1, kVarClip = 2, kVarRuntime = -1;
 
+// The cSGHMC cycle-init collects (m1 = theta, m2 written, nothing of the
+// moments read) at depth 1 take the plain sweep's per-run loop too: same
+// process, builds alternating (profiles/round6/ab_csg_per_run/), the Welford
+// init 1.5814 vs 1.5913 ms and 1.5697 vs 1.5843 (flat / per-tensor
+// gradients, each build's best geometry); the steady collect ran 3.5-5 %
+// slower that way at 1 x 1 and keeps the per-iteration lookup.
+template <int COLLECT, int UNROLL>
+constexpr bool csg_collect_per_run() {
+  return UNROLL == 1 &&
+         (COLLECT == BDL_COLLECT_WELFORD_INIT || COLLECT == BDL_COLLECT_MEAN_INIT);
+}
+
 // The launch's per-step constants (flags, clip coefficient, reciprocals).
 template <int METHOD, int COLLECT, int VAR, class A>
 __device__ __forceinline__ StepConst make_step_const(const A& a) {
@@ -867,7 +879,8 @@ __device__ __forceinline__ void step_body(const KArgs& a) {
     else
       chunk_slow<METHOD, NOISE, COLLECT, RECIP, UNROLL>(fa, fc, gb, gend, r, bad);
   }
-  } else if constexpr (!is_csghmc_sweep<METHOD>() || COLLECT != BDL_COLLECT_NONE) {
+  } else if constexpr (!is_csghmc_sweep<METHOD>() ||
+                       (COLLECT != BDL_COLLECT_NONE && !csg_collect_per_run<COLLECT, UNROLL>())) {
   for (int64_t gb = g0; gb < g1; gb += gstep) {
     while (r < a.nruns - 1 && run_end(r) <= gb * 4) ++r;
     const int64_t gend = min(gb + kIter, g1);
